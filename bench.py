@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: batched 1D c2c FFT N=2^20 (BASELINE.json configs[1]) on MI355X.
+
+A "step" is one hsfft_exec_batched over the per-GPU batch (4096 x 2^20 complex f64, inputs
+already resident in HBM).  Multi-GPU: one process per GPU (torch.distributed.run); each rank
+transforms its own 4096 rows (weak scaling, no data-path collective -- the path shards by
+batch index); rank 0 prints one JSON line with the max-over-ranks time.
+
+Other configs for development: --config c3 (12600 x 65536), c4 (Bluestein 99991 x 8192),
+c5 (r2c 2^22 x 32768 over the job, chunked per GPU).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "mixed-radix-fast-fourier-transform_amd")
+sys.path.insert(0, PKG)
+
+import hsfft  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+CONFIGS = {
+    # name: (kind, N, per-GPU batch, seed, description)
+    "c2": ("c2c", 1 << 20, 4096, 0x5EED0002, "batched c2c N=2^20, batch=4096 per GPU, fp64"),
+    "c3": ("c2c", 12600, 65536, 0x5EED0003, "mixed-radix c2c N=12600, batch=65536 per GPU, fp64"),
+    "c4": ("c2c", 99991, 8192, 0x5EED0004, "Bluestein c2c N=99991, batch=8192 per GPU, fp64"),
+    "c5": ("r2c", 1 << 22, 4096, 0x5EED0005, "r2c N=2^22, 4096 rows per GPU (32768 over 8 GPUs), fp64"),
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+class Comm:
+    """Barrier + max-reduce across ranks.  The FFT path has no exchange step, so the only
+    communication is control: gloo over TCP (no GPU buffers are involved)."""
+
+    def __init__(self, ws):
+        self.ws = ws
+        self.dist = None
+        if ws > 1:
+            import torch
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist, self.torch = dist, torch
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v):
+        if not self.dist:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, seconds_target=15.0):
+    """The reference (oracle/_ref, compiled from the unmodified sources) timed on host cores
+    over a bounded sample; falls back to the oracle restatement ('port') if absent."""
+    kind, n, _, seed, _ = cfg
+    threads = max(1, min(16, os.cpu_count() or 1))
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
+    sample = {("c2c", 1 << 20): 128, ("c2c", 12600): 8192, ("c2c", 99991): 64, ("r2c", 1 << 22): 32}.get((kind, n), 64)
+    if os.path.exists(ref_so):
+        L = ctypes.CDLL(ref_so)
+        L.hsref_time_batch.restype = ctypes.c_double
+        L.hsref_time_batch.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64]
+        secs = L.hsref_time_batch(n, 1, 1 if kind == "r2c" else 0, sample, threads, seed)
+        src = "reference"
+    else:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import numpy as np
+
+        import hsfft_testlib as T
+        lib = T.oracle()
+        if kind == "r2c":
+            x = T.real_input(n, seed, batch=sample).reshape(sample, n)
+            rp = lib.orc_real_create(n, 1, 0)
+            y = np.zeros((sample, n), dtype=np.complex128)
+            t0 = time.perf_counter()
+            lib.orc_r2c_batch(rp, T.ptr(x), T.ptr(y), sample, threads)
+            secs = time.perf_counter() - t0
+            lib.orc_real_destroy(rp)
+        else:
+            x = T.complex_input(n, seed, batch=sample).reshape(sample, n)
+            p = lib.orc_plan_create(n, 1, 0)
+            y = np.zeros_like(x)
+            t0 = time.perf_counter()
+            lib.orc_exec_batch(p, T.ptr(x), T.ptr(y), sample, threads)
+            secs = time.perf_counter() - t0
+            lib.orc_plan_destroy(p)
+        src = "port"
+    return {"value": round(n * sample / secs / 1e9, 6), "unit": "GSamples/s", "cores": threads, "kind": src,
+            "sample": f"{sample} transforms of N={n} ({kind}), {threads} threads, one plan per thread, "
+                      f"{secs:.2f} s wall"}
+
+
+def read_traffic(cfg_name):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
+    FETCH_SIZE x2 [gfx950 calibration] + WRITE_SIZE, per MI355X_MICROARCH.md §HBM)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(cfg_name)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch (development only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    comm = Comm(ws)
+    L = hsfft.lib()
+    ndev = hsfft.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    hsfft.check(L.hsfft_set_device(local % ndev), "set_device")
+
+    cfg = CONFIGS[args.config]
+    kind, n, batch, seed, desc = cfg
+    if args.batch:
+        batch = args.batch
+    samples = n * batch
+    if kind == "c2c":
+        plan = hsfft.Plan(n, 1)
+        din = hsfft.DeviceBuffer(samples * 16)
+        dout = hsfft.DeviceBuffer(samples * 16)
+        hsfft.fill_complex(din, samples, seed, rank * samples)
+        run = lambda: hsfft.exec_batched(plan, din, dout, batch)  # noqa: E731
+        bytes_per_sample = 32  # read 16 B + write 16 B
+        dtype = "f64 (complex128)"
+    else:
+        plan = hsfft.RealPlan(n, 1)
+        din = hsfft.DeviceBuffer(samples * 8)
+        dout = hsfft.DeviceBuffer(samples * 16)
+        hsfft.fill_real(din, samples, seed, rank * samples)
+        run = lambda: hsfft.r2c_batched(plan, din, dout, batch)  # noqa: E731
+        bytes_per_sample = 24  # read 8 B + write 16 B of the mirrored output
+        dtype = "f64"
+    hsfft.synchronize()
+
+    for _ in range(args.warmup):
+        run()
+    hsfft.synchronize()
+
+    comm.barrier()
+    hsfft.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    hsfft.synchronize()
+    comm.barrier()
+    t1 = time.perf_counter()
+    wall = comm.max(t1 - t0)
+
+    # HIP-event timing on the library stream (what the kernels take) + per-pass breakdown
+    npass = 0
+    pass_ms = []
+    if kind == "c2c":
+        ev_ms, pms = hsfft.time_batched(plan, din, dout, batch, max(1, args.steps))
+        npass = plan.num_passes()
+        pass_ms = [p for p in pms[:npass] if p >= 0]
+    else:
+        ev_ms = hsfft.time_r2c_batched(plan, din, dout, batch, max(1, args.steps))
+    ev_step_ms = comm.max(ev_ms / max(1, args.steps))
+
+    ms_per_step = wall / args.steps * 1e3
+    value = samples * ws / (ms_per_step / 1e3) / 1e9
+    out = {
+        "metric": "GSamples/s + achieved HBM GB/s, batched 1D c2c FFT N=2^20 at 1/2/4/8 MI355X"
+        if args.config == "c2" else f"GSamples/s ({desc})",
+        "value": round(value, 3),
+        "unit": "GSamples/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic (splitmix64 uniform [-1,1), generated in HBM)",
+        "config": {"workload": desc, "N": n, "per_gpu_batch": batch, "global_batch": batch * ws,
+                   "parallelism": f"batch-sharded x{ws} (no collective)", "passes": npass},
+        "achieved_hbm_gbs": round(samples * bytes_per_sample * ws / (ms_per_step / 1e3) / 1e9, 1),
+        "event_ms_per_step": round(ev_step_ms, 4),
+    }
+    if pass_ms:
+        dom = max(range(len(pass_ms)), key=lambda i: pass_ms[i])
+        ach = samples * bytes_per_sample / (pass_ms[dom] / 1e3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config),
+                           "kernel": f"pass {dom} of {npass}", "pass_ms": [round(p, 4) for p in pass_ms]}
+    else:
+        ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config),
+                           "kernel": "whole step (event timed)"}
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    din.free()
+    dout.free()
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,94 @@
+/*
+ * hsfft_gpu.h -- MI355X extension API of libhsfft.so (no counterpart in the reference, which
+ * has no batched or device-resident entry points).
+ *
+ * Conventions: plain pointers and sizes only.  "d_" pointers are device (HBM) pointers
+ * obtained from hsfft_malloc (or any hipMalloc'd memory).  Batched transforms use contiguous
+ * rows (row b starts at b*N samples).  Calls are asynchronous on the library stream of the
+ * current device unless stated; hsfft_synchronize() waits.  Functions return 0 on success
+ * and a negative code on error (message via hsfft_last_error()).
+ */
+#ifndef HSFFT_GPU_H_
+#define HSFFT_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "highspeedFFT.h"
+#include "real.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSFFT_OK 0
+#define HSFFT_ERR_ARG -1
+#define HSFFT_ERR_DEVICE -2
+#define HSFFT_ERR_NOMEM -3
+#define HSFFT_ERR_UNSUPPORTED -4
+
+/* --- devices, memory, streams ---------------------------------------------------------- */
+int hsfft_device_count(void);
+int hsfft_set_device(int dev);          /* also selects the library stream of that device */
+int hsfft_get_device(void);
+void *hsfft_malloc(size_t bytes);        /* device memory on the current device, NULL on error */
+int hsfft_free(void *d_ptr);
+int hsfft_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes);  /* synchronous */
+int hsfft_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes);  /* synchronous */
+int hsfft_memset(void *d_ptr, int value, size_t bytes);
+int hsfft_synchronize(void);
+void *hsfft_get_stream(void);            /* hipStream_t of the current device */
+const char *hsfft_last_error(void);
+
+/* --- plan options ---------------------------------------------------------------------- */
+/* Twiddle mode for plans created afterwards by fft_init/fft_real_init on this thread:
+ *   0 = reference (default): byte-identical to the reference planner, including its
+ *       twiddle-table quirk;
+ *   1 = exact: every stage twiddle from sincos (D2 fixed).
+ * The environment variable HSFFT_TWIDDLE=exact sets the process default. */
+int hsfft_set_twiddle_mode(int mode);
+int hsfft_get_twiddle_mode(void);
+/* Re-upload the plan's public twiddle array after the caller modified it in place. */
+int hsfft_plan_refresh(fft_object obj);
+/* Number of GPU passes (kernel launches per transform batch) the plan executes. */
+int hsfft_plan_num_passes(fft_object obj);
+/* Digit-reversal map of the reference recursion: output slot q holds input index map[q]
+ * after the leaf stage (integer exact; N entries; mixed-radix plans only). */
+int hsfft_digit_reverse_map(fft_object obj, int *map);
+
+/* --- batched, device-resident execution ------------------------------------------------ */
+/* c2c: d_in, d_out hold batch*N complex; d_in is not modified; d_in != d_out. */
+int hsfft_exec_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch);
+/* r2c in the reference layout: batch rows of N reals -> batch rows of N complex (mirrored) */
+int hsfft_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out, int batch);
+/* c2r: batch rows of N complex (first N/2+1 read) -> batch rows of N reals */
+int hsfft_c2r_batched(fft_real_object obj, const fft_data *d_in, fft_type *d_out, int batch);
+/* batched linear/circular convolution of equal-length real rows (reference semantics of
+ * fft_convolve, applied row-wise); returns the output length per row, or < 0 */
+int hsfft_convolve_batched(const char *type, const char *conv_type, const fft_type *d_a,
+                           int length1, const fft_type *d_b, int length2, fft_type *d_out,
+                           int batch);
+
+/* --- synthetic data and timing (benchmark support) ------------------------------------- */
+/* x[j] = (u(2(offset+j)), u(2(offset+j)+1)), u(i) = splitmix64(seed ^ i) -> [-1, 1) */
+int hsfft_fill_complex(fft_data *d_x, int64_t count, uint64_t seed, uint64_t offset);
+int hsfft_fill_real(fft_type *d_x, int64_t count, uint64_t seed, uint64_t offset);
+/* Runs hsfft_exec_batched `iters` times between HIP events on the library stream and
+ * returns the total milliseconds in *ms; per-pass average kernel milliseconds (measured
+ * with events around each pass, one extra instrumented iteration) go to pass_ms[0..npass) */
+int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch,
+                       int iters, float *ms, float *pass_ms, int max_pass);
+int hsfft_time_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out,
+                           int batch, int iters, float *ms);
+
+/* --- multi-device (single process; one host thread per device, no collective) --------- */
+/* Shards the batch contiguously over devices 0..ndev-1: h-side arrays of per-device
+ * pointers d_in[g], d_out[g] each hold rows [g*batch/ndev, (g+1)*batch/ndev). */
+int hsfft_exec_multi(fft_object obj, const fft_data *const *d_in, fft_data *const *d_out,
+                     int batch, int ndev);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HSFFT_GPU_H_ */

@@ -1,0 +1,571 @@
+/*
+ * hsfft_device.hip -- HIP/CDNA4 (gfx950) device layer of libhsfft.so.
+ *
+ * Kernels
+ *   k_pass_generic : one fused Stockham pass (any radix list, LDS ping-pong).  Replaces the
+ *                    recursion + combine loops of mixed_radix_dit_rec (ref
+ *                    src/highSpeedFFT.c:318-1629) for one range of stages.
+ *   k_pass_r8      : hsfft_pass_r8.h -- register-resident radix-8 passes (hot path).
+ *   k_fill_*       : splitmix64 synthetic inputs (bench / tests).
+ *   k_r2c_post / k_c2r_pre : real-signal split / merge (ref src/real.c:108-132, :169-179).
+ *   k_cmul / k_scale_real / k_copy_rows : convolution helpers (ref src/convolve.c:137-160).
+ *
+ * Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction: the results
+ * must be bit-identical to the reference's separately rounded multiplies and adds).
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include "hsfft_butterfly.h"
+#include "hsfft_internal.h"
+
+namespace {
+
+thread_local char g_err[512];
+hipStream_t g_stream[HS_MAX_DEV];
+bool g_stream_init[HS_MAX_DEV];
+
+int set_err(hipError_t e, const char *what)
+{
+    snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+    return -2;
+}
+
+#define HCHK(call)                                                      \
+    do {                                                                \
+        hipError_t e_ = (call);                                         \
+        if (e_ != hipSuccess) return set_err(e_, #call);                \
+    } while (0)
+
+hipStream_t stream()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) dev = 0;
+    if (!g_stream_init[dev]) {
+        if (hipStreamCreateWithFlags(&g_stream[dev], hipStreamNonBlocking) != hipSuccess) g_stream[dev] = 0;
+        g_stream_init[dev] = true;
+    }
+    return g_stream[dev];
+}
+
+/* ------------------------------------------------------------------ generic pass kernel */
+struct KArgs {
+    const double2 *in;
+    double2 *out;
+    const double2 *tw;
+    const double *gcs;
+    const double2 *laux, *saux;
+    long long idist, odist, A, B, nsig, tiles_q, tiles;
+    int P, nst, leaf, Wm, Wq, G;
+    int sgn, dir, conj, load_op, store_op;
+    int radix[HS_MAX_PASS_STAGES];
+    int gcs_off[HS_MAX_PASS_STAGES];
+};
+
+__device__ __forceinline__ double2 hook_load(const KArgs &a, const double2 *in, long long n)
+{
+    if (a.load_op == HS_LOAD_CHIRP) {
+        if (n >= a.nsig) return make_double2(0.0, 0.0);
+        double2 x = in[n], h = a.laux[n];
+        if (a.dir == 1) return make_double2(x.x * h.x + x.y * h.y, -x.x * h.y + x.y * h.x);
+        return make_double2(x.x * h.x - x.y * h.y, x.x * h.y + x.y * h.x);
+    }
+    return in[n];
+}
+
+__device__ __forceinline__ void hook_store(const KArgs &a, double2 *out, long long n, double2 y)
+{
+    if (a.store_op == HS_STORE_SPEC) {
+        double2 k = a.saux[n];
+        if (a.dir == 1) {
+            double t = y.x * k.x - y.y * k.y;
+            y.y = y.x * k.y + y.y * k.x;
+            y.x = t;
+        } else {
+            double t = y.x * k.x + y.y * k.y;
+            y.y = -y.x * k.y + y.y * k.x;
+            y.x = t;
+        }
+        out[n] = y;
+    } else if (a.store_op == HS_STORE_CHIRP) {
+        if (n >= a.nsig) return;
+        double2 h = a.saux[n];
+        if (a.dir == 1) out[n] = make_double2(y.x * h.x + y.y * h.y, -y.x * h.y + y.y * h.x);
+        else out[n] = make_double2(y.x * h.x - y.y * h.y, y.x * h.y + y.y * h.x);
+    } else {
+        out[n] = y;
+    }
+}
+
+template <int R>
+__device__ void stage_fixed(const KArgs &a, const double2 *src, double2 *dst, int Lloc, bool leaf,
+                            long long m0, long long q0)
+{
+    const int P = a.P, G = a.G;
+    const int S = P / (Lloc * R);
+    const int nb = (P / R) * G;
+    const long long L = a.B * Lloc;
+    for (int bf = threadIdx.x; bf < nb; bf += blockDim.x) {
+        const int gi = bf % G, j = bf / G;
+        const int kloc = j % Lloc, ml = j / Lloc;
+        double xr[R], xi[R];
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            double2 v = src[((ml + i * S) * Lloc + kloc) * G + gi];
+            xr[i] = v.x;
+            xi[i] = v.y;
+        }
+        if (!leaf) {
+            const long long q = q0 + gi % a.Wq, m = m0 + gi / a.Wq;
+            const long long k = q + a.B * kloc;
+            const bool skip = ((R == 4 || R == 5 || R == 7) && k == 0) || q >= a.B || m >= a.A;
+            if (!skip) {
+                const double2 *w = a.tw + (L - 1 + (long long)(R - 1) * k);
+#pragma unroll
+                for (int i = 1; i < R; i++) {
+                    double2 t = w[i - 1];
+                    hsb::twmul(xr[i], xi[i], t.x, a.conj ? -t.y : t.y);
+                }
+            }
+        }
+        hsb::bfly<R>(xr, xi, a.sgn, leaf);
+#pragma unroll
+        for (int jj = 0; jj < R; jj++) dst[(ml * Lloc * R + kloc + jj * Lloc) * G + gi] = make_double2(xr[jj], xi[jj]);
+    }
+}
+
+__device__ void stage_odd(const KArgs &a, const double2 *src, double2 *dst, int R, int Lloc,
+                          const double *cs, long long m0, long long q0)
+{
+    const int P = a.P, G = a.G;
+    const int S = P / (Lloc * R);
+    const int nb = (P / R) * G;
+    const long long L = a.B * Lloc;
+    for (int bf = threadIdx.x; bf < nb; bf += blockDim.x) {
+        const int gi = bf % G, j = bf / G;
+        const int kloc = j % Lloc, ml = j / Lloc;
+        double xr[64], xi[64];
+        for (int i = 0; i < R; i++) {
+            double2 v = src[((ml + i * S) * Lloc + kloc) * G + gi];
+            xr[i] = v.x;
+            xi[i] = v.y;
+        }
+        const long long q = q0 + gi % a.Wq, m = m0 + gi / a.Wq;
+        if (q < a.B && m < a.A) { /* odd radices multiply every column, k = 0 included (:1552-1560) */
+            const long long k = q + a.B * kloc;
+            const double2 *w = a.tw + (L - 1 + (long long)(R - 1) * k);
+            for (int i = 1; i < R; i++) {
+                double2 t = w[i - 1];
+                hsb::twmul(xr[i], xi[i], t.x, a.conj ? -t.y : t.y);
+            }
+        }
+        hsb::bfly_odd(xr, xi, R, a.sgn, cs, cs + (R - 1));
+        for (int jj = 0; jj < R; jj++) dst[(ml * Lloc * R + kloc + jj * Lloc) * G + gi] = make_double2(xr[jj], xi[jj]);
+    }
+}
+
+template <bool ODD>
+__global__ __launch_bounds__(256) void k_pass_generic(KArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const long long blk = blockIdx.x;
+    const long long b = blk / a.tiles, tile = blk % a.tiles;
+    const long long m0 = (tile / a.tiles_q) * a.Wm, q0 = (tile % a.tiles_q) * a.Wq;
+    const double2 *in = a.in + b * a.idist;
+    double2 *out = a.out + b * a.odist;
+    const int P = a.P, G = a.G;
+    double2 *src = lds, *dst = lds + P * G;
+
+    for (int e = threadIdx.x; e < P * G; e += blockDim.x) {
+        const int gi = e % G, t = e / G;
+        const long long m = m0 + gi / a.Wq, q = q0 + gi % a.Wq;
+        double2 v = make_double2(0.0, 0.0);
+        if (m < a.A && q < a.B) v = hook_load(a, in, ((long long)t * a.A + m) * a.B + q);
+        src[t * G + gi] = v;
+    }
+    __syncthreads();
+
+    int Lloc = 1;
+    for (int s = 0; s < a.nst; s++) {
+        const int r = a.radix[s];
+        const bool leaf = a.leaf && s == 0;
+        switch (r) {
+        case 2: stage_fixed<2>(a, src, dst, Lloc, leaf, m0, q0); break;
+        case 3: stage_fixed<3>(a, src, dst, Lloc, leaf, m0, q0); break;
+        case 4: stage_fixed<4>(a, src, dst, Lloc, leaf, m0, q0); break;
+        case 5: stage_fixed<5>(a, src, dst, Lloc, leaf, m0, q0); break;
+        case 7: stage_fixed<7>(a, src, dst, Lloc, leaf, m0, q0); break;
+        case 8: stage_fixed<8>(a, src, dst, Lloc, leaf, m0, q0); break;
+        default:
+            if constexpr (ODD) stage_odd(a, src, dst, r, Lloc, a.gcs + a.gcs_off[s], m0, q0);
+            break;
+        }
+        __syncthreads();
+        double2 *t = src;
+        src = dst;
+        dst = t;
+        Lloc *= r;
+    }
+
+    for (int e = threadIdx.x; e < P * G; e += blockDim.x) {
+        const int qi = e % a.Wq, rest = e / a.Wq;
+        const int u = rest % P, mi = rest / P;
+        const long long m = m0 + mi, q = q0 + qi;
+        if (m < a.A && q < a.B) hook_store(a, out, (m * P + u) * a.B + q, src[u * G + mi * a.Wq + qi]);
+    }
+}
+
+/* ------------------------------------------------------------------ helpers */
+__device__ __forceinline__ double splitmix_u(unsigned long long seed, unsigned long long i)
+{
+    unsigned long long z = (seed ^ i) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (1.0 / 4503599627370496.0) - 1.0;
+}
+
+__global__ void k_fill_complex(double2 *x, long long count, unsigned long long seed, unsigned long long off)
+{
+    for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < count; j += (long long)gridDim.x * blockDim.x) {
+        unsigned long long e = (unsigned long long)j + off;
+        x[j] = make_double2(splitmix_u(seed, 2 * e), splitmix_u(seed, 2 * e + 1));
+    }
+}
+
+__global__ void k_fill_real(double *x, long long count, unsigned long long seed, unsigned long long off)
+{
+    for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < count; j += (long long)gridDim.x * blockDim.x)
+        x[j] = splitmix_u(seed, (unsigned long long)j + off);
+}
+
+/* ref real.c:108-132 */
+__global__ void k_r2c_post(const double2 *Z, const double2 *w2, double2 *X, int h, long long zdist, long long xdist)
+{
+    const int b = blockIdx.y;
+    const double2 *z = Z + b * zdist;
+    double2 *x = X + b * xdist;
+    const int N = 2 * h;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= h; k += gridDim.x * blockDim.x) {
+        if (k == 0) {
+            double2 z0 = z[0];
+            x[0] = make_double2(z0.x + z0.y, 0.0);
+            x[h] = make_double2(z0.x - z0.y, 0.0);
+        } else if (k < h) {
+            const double2 a = z[k], c = z[h - k], w = w2[k];
+            const double t1 = a.y + c.y, t2 = c.x - a.x;
+            const double re = (a.x + c.x + (t1 * w.x) + (t2 * w.y)) / 2.0;
+            const double im = (a.y - c.y + (t2 * w.x) - (t1 * w.y)) / 2.0;
+            x[k] = make_double2(re, im);
+            x[N - k] = make_double2(re, -im);
+        }
+    }
+}
+
+/* ref real.c:169-179 */
+__global__ void k_c2r_pre(const double2 *X, const double2 *w2, double2 *Zi, int h, long long xdist, long long zdist)
+{
+    const int b = blockIdx.y;
+    const double2 *x = X + b * xdist;
+    double2 *z = Zi + b * zdist;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < h; k += gridDim.x * blockDim.x) {
+        const double2 a = x[k], c = x[h - k], w = w2[k];
+        const double t1 = -a.y - c.y, t2 = -c.x + a.x;
+        z[k] = make_double2(a.x + c.x + (t1 * w.x) - (t2 * w.y), a.y - c.y + (t2 * w.x) + (t1 * w.y));
+    }
+}
+
+/* ref convolve.c:147-151 */
+__global__ void k_cmul(const double2 *A, const double2 *Bv, double2 *C, long long n, long long dist)
+{
+    const long long b = blockIdx.y;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const double2 a = A[b * dist + i], c = Bv[b * dist + i];
+        C[b * dist + i] = make_double2(a.x * c.x - a.y * c.y, a.x * c.y + a.y * c.x);
+    }
+}
+
+/* ref convolve.c:157-160 */
+__global__ void k_scale_real(double *x, long long n, long long dist, double divisor)
+{
+    const long long b = blockIdx.y;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        x[b * dist + i] /= divisor;
+}
+
+/* row copy with zero fill: dst[b][i] = i < ncopy ? src[b][soff + i] : 0 for i < dlen
+ * (zero padding of convolve.c:117-140 and the output slice of :163-201) */
+__global__ void k_copy_rows(const double *src, long long sdist, long long soff, long long ncopy, double *dst,
+                            long long ddist, long long dlen)
+{
+    const long long b = blockIdx.y;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < dlen; i += (long long)gridDim.x * blockDim.x)
+        dst[b * ddist + i] = i < ncopy ? src[b * sdist + soff + i] : 0.0;
+}
+
+hipEvent_t g_t0, g_t1;
+bool g_timer_init = false;
+hipEvent_t g_pev[2 * HS_MAX_PASSES];
+bool g_pev_init = false;
+
+int grid_for(long long n, int threads)
+{
+    long long g = (n + threads - 1) / threads;
+    if (g > 65535) g = 65535;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+#include "hsfft_pass_r8.h"
+
+extern "C" {
+
+int hsd_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int hsd_set_device(int dev)
+{
+    HCHK(hipSetDevice(dev));
+    (void)stream();
+    return 0;
+}
+
+int hsd_get_device(void)
+{
+    int d = -1;
+    if (hipGetDevice(&d) != hipSuccess) return -1;
+    return d;
+}
+
+void *hsd_malloc(size_t bytes)
+{
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+        set_err(e, "hipMalloc");
+        return nullptr;
+    }
+    return p;
+}
+
+int hsd_free(void *p)
+{
+    if (p) HCHK(hipFree(p));
+    return 0;
+}
+
+int hsd_h2d(void *d, const void *h, size_t bytes)
+{
+    HCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream()));
+    HCHK(hipStreamSynchronize(stream()));
+    return 0;
+}
+
+int hsd_d2h(void *h, const void *d, size_t bytes)
+{
+    HCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream()));
+    HCHK(hipStreamSynchronize(stream()));
+    return 0;
+}
+
+int hsd_d2d_async(void *d, const void *s, size_t bytes)
+{
+    HCHK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, stream()));
+    return 0;
+}
+
+int hsd_memset_async(void *d, int v, size_t bytes)
+{
+    HCHK(hipMemsetAsync(d, v, bytes, stream()));
+    return 0;
+}
+
+int hsd_sync(void)
+{
+    HCHK(hipStreamSynchronize(stream()));
+    return 0;
+}
+
+void *hsd_stream(void) { return (void *)stream(); }
+
+int hsd_is_device_ptr(const void *p)
+{
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof at);
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+const char *hsd_errstr(void) { return g_err; }
+
+int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
+{
+    if (p->variant == HS_KV_R8X3) return r8::launch(p, l, stream());
+    KArgs a;
+    memset(&a, 0, sizeof a);
+    a.in = (const double2 *)l->in;
+    a.out = (double2 *)l->out;
+    a.tw = (const double2 *)l->tw;
+    a.gcs = l->gcs;
+    a.laux = (const double2 *)l->load_aux;
+    a.saux = (const double2 *)l->store_aux;
+    a.idist = l->idist;
+    a.odist = l->odist;
+    a.A = p->A;
+    a.B = p->B;
+    a.nsig = l->nsig;
+    a.P = p->P;
+    a.nst = p->nst;
+    a.leaf = p->leaf;
+    a.Wm = p->Wm;
+    a.Wq = p->Wq;
+    a.G = p->G;
+    a.sgn = l->sgn;
+    a.dir = l->dir;
+    a.conj = l->conj;
+    a.load_op = l->load_op;
+    a.store_op = l->store_op;
+    for (int s = 0; s < p->nst; s++) {
+        a.radix[s] = p->radix[s];
+        a.gcs_off[s] = p->gcs_off[s];
+    }
+    long long tm = (p->A + p->Wm - 1) / p->Wm, tq = (p->B + p->Wq - 1) / p->Wq;
+    a.tiles_q = tq;
+    a.tiles = tm * tq;
+    long long grid = a.tiles * l->batch;
+    size_t lds = 2 * (size_t)p->P * p->G * sizeof(double2);
+    if (grid <= 0 || grid > 0x7fffffffLL || lds > 65536) {
+        snprintf(g_err, sizeof g_err, "hsd_run_pass: bad launch geometry (grid %lld, lds %zu)", grid, lds);
+        return -1;
+    }
+    bool odd = false;
+    for (int s = 0; s < p->nst; s++) {
+        const int r = p->radix[s];
+        odd |= !(r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8);
+    }
+    if (odd) hipLaunchKernelGGL(k_pass_generic<true>, dim3((unsigned)grid), dim3(256), lds, stream(), a);
+    else hipLaunchKernelGGL(k_pass_generic<false>, dim3((unsigned)grid), dim3(256), lds, stream(), a);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset)
+{
+    hipLaunchKernelGGL(k_fill_complex, dim3(4096), dim3(256), 0, stream(), (double2 *)d, (long long)count,
+                       (unsigned long long)seed, (unsigned long long)offset);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset)
+{
+    hipLaunchKernelGGL(k_fill_real, dim3(4096), dim3(256), 0, stream(), (double *)d, (long long)count,
+                       (unsigned long long)seed, (unsigned long long)offset);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_r2c_post, dim3(grid_for(h + 1, 256), batch), dim3(256), 0, stream(), (const double2 *)Z,
+                       (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_c2r_pre(const void *X, const void *tw2, void *Zin, int h, int batch, long long xdist, long long zdist)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_c2r_pre, dim3(grid_for(h, 256), batch), dim3(256), 0, stream(), (const double2 *)X,
+                       (const double2 *)tw2, (double2 *)Zin, h, xdist, zdist);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_cmul(const void *A, const void *Bv, void *C, long long n, int batch, long long dist)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_cmul, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (const double2 *)A,
+                       (const double2 *)Bv, (double2 *)C, n, dist);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_scale_real(void *x, long long n, int batch, long long dist, double divisor)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_scale_real, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (double *)x, n, dist, divisor);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
+                  long long dlen, int batch)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(dlen, 256), batch), dim3(256), 0, stream(), (const double *)src,
+                       sdist, soff, ncopy, (double *)dst, ddist, dlen);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_timer_start(void)
+{
+    if (!g_timer_init) {
+        HCHK(hipEventCreate(&g_t0));
+        HCHK(hipEventCreate(&g_t1));
+        g_timer_init = true;
+    }
+    HCHK(hipEventRecord(g_t0, stream()));
+    return 0;
+}
+
+int hsd_timer_stop(float *ms)
+{
+    HCHK(hipEventRecord(g_t1, stream()));
+    HCHK(hipEventSynchronize(g_t1));
+    HCHK(hipEventElapsedTime(ms, g_t0, g_t1));
+    return 0;
+}
+
+int hsd_pass_timer_begin(int i)
+{
+    if (!g_pev_init) {
+        for (int k = 0; k < 2 * HS_MAX_PASSES; k++) HCHK(hipEventCreate(&g_pev[k]));
+        g_pev_init = true;
+    }
+    if (i < 0 || i >= HS_MAX_PASSES) return -1;
+    HCHK(hipEventRecord(g_pev[2 * i], stream()));
+    return 0;
+}
+
+int hsd_pass_timer_end(int i)
+{
+    if (i < 0 || i >= HS_MAX_PASSES) return -1;
+    HCHK(hipEventRecord(g_pev[2 * i + 1], stream()));
+    return 0;
+}
+
+int hsd_pass_timer_read(int n, float *ms)
+{
+    for (int i = 0; i < n && i < HS_MAX_PASSES; i++) {
+        HCHK(hipEventSynchronize(g_pev[2 * i + 1]));
+        HCHK(hipEventElapsedTime(&ms[i], g_pev[2 * i], g_pev[2 * i + 1]));
+    }
+    return 0;
+}
+
+}  // extern "C"

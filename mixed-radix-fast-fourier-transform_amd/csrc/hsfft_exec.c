@@ -1,0 +1,685 @@
+/*
+ * hsfft_exec.c -- execution side of libhsfft.so (host C): plan registry, Stockham pass
+ * scheduling, the drop-in fft_exec (ref src/highSpeedFFT.c:1920-1942), the Bluestein
+ * orchestration (ref :1735-1907) and the batched / device-pointer extension API.
+ *
+ * There is no CPU compute path: every transform runs on the GPU through the device layer.
+ * Without a usable GPU the compute entry points fail loudly (stderr + exit for the drop-in
+ * functions, the reference's error convention; an error code for the extension API).
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hsfft_gpu.h"
+#include "hsfft_host.h"
+
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static hs_entry *g_entries;
+static __thread char g_errbuf[512];
+
+void hs_seterr(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_errbuf, sizeof g_errbuf, fmt, ap);
+    va_end(ap);
+}
+
+const char *hsfft_last_error(void) { return g_errbuf; }
+
+static void fatal(const char *what)
+{
+    fprintf(stderr, "Error: %s (%s)\n", what, g_errbuf[0] ? g_errbuf : hsd_errstr());
+    exit(EXIT_FAILURE);
+}
+
+int hs_require_gpu(void)
+{
+    static int ndev = -1;
+    if (ndev < 0) ndev = hsd_device_count();
+    if (ndev <= 0) {
+        hs_seterr("no HIP device available: libhsfft has no CPU execution path");
+        return HSFFT_ERR_DEVICE;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ scheduling */
+static int is_leaf_len(int n) { return n == 2 || n == 3 || n == 4 || n == 5 || n == 7 || n == 8; }
+
+/* Effective stage list of the reference recursion: descend with data_length = M taking
+ * factors[fi]; a data_length in {2,3,4,5,7,8} is a leaf butterfly of that size (ref
+ * :332-713 dispatch on data_length before radix).  Returns stages innermost first. */
+static int effective_stages(int M, const int *fac, int lf, int *out, int *first_leaf)
+{
+    int outer[HS_MAX_STAGES], n = 0, len = M, fi = 0;
+    *first_leaf = 0;
+    while (len > 1) {
+        if (is_leaf_len(len)) {
+            outer[n++] = len;
+            *first_leaf = 1;
+            break;
+        }
+        if (fi >= lf || fac[fi] <= 1 || len % fac[fi] != 0 || n >= HS_MAX_STAGES) return -1;
+        outer[n++] = fac[fi];
+        len /= fac[fi++];
+    }
+    for (int i = 0; i < n; i++) out[i] = outer[n - 1 - i];
+    return n;
+}
+
+static int pass_pmax(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *s = getenv("HSFFT_PMAX");
+        v = s ? atoi(s) : 512;
+        if (v < 8) v = 8;
+    }
+    return v;
+}
+
+/* Groups stages into passes of at most Pmax points and chooses the tile so that global
+ * loads/stores move >= 128 contiguous bytes (8 complex) per row where the shape allows. */
+static int build_passes(hs_entry *e)
+{
+    const int pmax = pass_pmax();
+    int s = 0, np = 0;
+    long long B = 1;
+    while (s < e->nst) {
+        if (np >= HS_MAX_PASSES) return -1;
+        hsd_pass *p = &e->pass[np];
+        memset(p, 0, sizeof *p);
+        p->P = 1;
+        p->leaf = (s == 0) && e->first_leaf;
+        while (s < e->nst && p->nst < HS_MAX_PASS_STAGES && (p->nst == 0 || (long long)p->P * e->stage_r[s] <= pmax)) {
+            p->radix[p->nst] = e->stage_r[s];
+            p->gcs_off[p->nst] = -1;
+            p->P *= e->stage_r[s];
+            p->nst++;
+            s++;
+        }
+        p->B = B;
+        p->A = e->M / (B * p->P);
+        int gmax = 2048 / p->P;
+        if (gmax < 1) gmax = 1;
+        int wq = (int)(B < 8 ? B : 8);
+        if (wq > gmax) wq = gmax;
+        int wm = 8 / wq;
+        if (wm * wq > gmax) wm = gmax / wq;
+        if (wm < 1) wm = 1;
+        if (wm > p->A) wm = (int)p->A;
+        p->Wq = wq;
+        p->Wm = wm;
+        p->G = wq * wm;
+        p->variant = HS_KV_GENERIC;
+        B *= p->P;
+        np++;
+    }
+    e->npass = np;
+    return 0;
+}
+
+/* odd-radix constants: cos/sin(i*PI2/p) for i <= (p-1)/2, mirrored (ref :1527-1541) */
+static int build_gcs(hs_entry *e)
+{
+    int total = 0;
+    for (int i = 0; i < e->npass; i++)
+        for (int s = 0; s < e->pass[i].nst; s++) {
+            int r = e->pass[i].radix[s];
+            if (r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8) continue;
+            if (r > 63) {
+                hs_seterr("radix %d exceeds the odd-radix kernel limit (63)", r);
+                return -1;
+            }
+            total += 2 * (r - 1);
+        }
+    e->ngcs = total;
+    e->gcs = total ? malloc(sizeof(double) * (size_t)total) : NULL;
+    int off = 0;
+    for (int i = 0; i < e->npass; i++)
+        for (int s = 0; s < e->pass[i].nst; s++) {
+            int r = e->pass[i].radix[s];
+            if (r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8) continue;
+            const int mid = (r - 1) / 2;
+            double *cs = e->gcs + off, *sn = cs + (r - 1);
+            for (int k = 1; k <= mid; k++) {
+                double sv, cv;
+                sincos(k * PI2 / r, &sv, &cv);
+                cs[k - 1] = cv;
+                sn[k - 1] = sv;
+            }
+            for (int k = 0; k < mid; k++) {
+                sn[k + mid] = -sn[mid - 1 - k];
+                cs[k + mid] = cs[mid - 1 - k];
+            }
+            e->pass[i].gcs_off[s] = off;
+            off += 2 * (r - 1);
+        }
+    return 0;
+}
+
+static void free_devstate(hs_devstate *d)
+{
+    if (!d) return;
+    hsd_free(d->d_tw);
+    hsd_free(d->d_gcs);
+    hsd_free(d->d_chirp);
+    hsd_free(d->d_hk);
+    free(d);
+}
+
+static void entry_free(hs_entry *e)
+{
+    int cur = hsd_get_device();
+    for (int d = 0; d < HS_MAX_DEV; d++)
+        if (e->ds[d]) {
+            hsd_set_device(d);
+            free_devstate(e->ds[d]);
+        }
+    if (cur >= 0) hsd_set_device(cur);
+    free(e->tw_private);
+    free(e->gcs);
+    free(e->chirp);
+    free(e);
+}
+
+static int snapshot_matches(const hs_entry *e, const struct fft_set *o)
+{
+    if (e->N != o->N || e->sgn != o->sgn || e->lt != o->lt || e->lf != o->lf) return 0;
+    for (int i = 0; i < o->lf && i < 64; i++)
+        if (e->factors[i] != o->factors[i]) return 0;
+    return 1;
+}
+
+static hs_entry *entry_build(const struct fft_set *o)
+{
+    if (o->lf < 0 || o->lf > 64) {
+        hs_seterr("plan has %d factors", o->lf);
+        return NULL;
+    }
+    hs_entry *e = calloc(1, sizeof *e);
+    e->key = o;
+    e->N = o->N;
+    e->sgn = o->sgn;
+    e->lt = o->lt;
+    e->lf = o->lf;
+    memcpy(e->factors, o->factors, sizeof e->factors);
+    memcpy(e->rfac, o->factors, sizeof e->rfac);
+    e->rlf = o->lf;
+    e->tw_from_struct = 1;
+    long long prod = 1;
+    for (int i = 0; i < o->lf; i++) prod *= o->factors[i];
+    if (o->lt == 0) {
+        e->M = o->N;
+    } else {
+        /* bluestein_fft runs at the log2 length; fft_init sized the plan with log10.  Where
+         * they disagree (N = 2^k+1, defect D5) the reference reads past its twiddles; here
+         * the exec-side length gets its own factorisation and twiddle table. */
+        e->M = hs_bluestein_M_exec(o->N);
+        if (prod != e->M) {
+            e->tw_from_struct = 0;
+            e->rlf = factors(e->M, e->rfac);
+            e->tw_private = calloc((size_t)e->M, sizeof(fft_data));
+            hs_longvector(e->tw_private, e->M, e->factors, e->lf, hs_twiddle_mode() == 1);
+            if (o->sgn == -1)
+                for (int i = 0; i < e->M; i++) e->tw_private[i].im = -e->tw_private[i].im;
+        }
+    }
+    if (e->M <= 0) {
+        hs_seterr("invalid transform length %d", e->M);
+        free(e);
+        return NULL;
+    }
+    if (e->M > 1) {
+        e->nst = effective_stages(e->M, e->rfac, e->rlf, e->stage_r, &e->first_leaf);
+        if (e->nst < 0) {
+            hs_seterr("factor list of the plan does not describe length %d", e->M);
+            free(e->tw_private);
+            free(e);
+            return NULL;
+        }
+        if (build_passes(e) || build_gcs(e)) {
+            free(e->tw_private);
+            free(e->gcs);
+            free(e);
+            return NULL;
+        }
+    }
+    if (o->lt == 1) { /* chirp h(n) = exp(i*pi*n^2/N), ref :1674-1690 */
+        const double PI = 3.1415926535897932384626433832795;
+        const int N = o->N;
+        e->chirp = malloc(sizeof(fft_data) * (size_t)N);
+        const double theta = PI / N;
+        int l2 = 0;
+        const int len2 = 2 * N;
+        for (int n = 0; n < N; n++) {
+            double sn, cs;
+            sincos(theta * l2, &sn, &cs);
+            e->chirp[n].re = cs;
+            e->chirp[n].im = sn;
+            l2 += 2 * n + 1;
+            while (l2 > len2) l2 -= len2;
+        }
+    }
+    return e;
+}
+
+hs_entry *hs_entry_get(const struct fft_set *obj)
+{
+    pthread_mutex_lock(&g_lock);
+    hs_entry **pp = &g_entries, *e = NULL;
+    for (; *pp; pp = &(*pp)->next)
+        if ((*pp)->key == obj) {
+            e = *pp;
+            break;
+        }
+    if (e && !snapshot_matches(e, obj)) { /* caller edited the public fields: rebuild */
+        *pp = e->next;
+        entry_free(e);
+        e = NULL;
+    }
+    if (!e) {
+        e = entry_build(obj);
+        if (e) {
+            e->next = g_entries;
+            g_entries = e;
+        }
+    }
+    pthread_mutex_unlock(&g_lock);
+    return e;
+}
+
+void hs_entry_release(const struct fft_set *obj)
+{
+    pthread_mutex_lock(&g_lock);
+    for (hs_entry **pp = &g_entries; *pp; pp = &(*pp)->next)
+        if ((*pp)->key == obj) {
+            hs_entry *e = *pp;
+            *pp = e->next;
+            entry_free(e);
+            break;
+        }
+    pthread_mutex_unlock(&g_lock);
+}
+
+/* ------------------------------------------------------------------ scratch */
+#define HS_NSCRATCH 8
+static void *g_scr[HS_MAX_DEV][HS_NSCRATCH];
+static size_t g_scr_sz[HS_MAX_DEV][HS_NSCRATCH];
+
+void *hs_scratch(int cls, size_t bytes)
+{
+    int d = hsd_get_device();
+    if (d < 0 || d >= HS_MAX_DEV || cls < 0 || cls >= HS_NSCRATCH) return NULL;
+    if (g_scr_sz[d][cls] < bytes) {
+        hsd_sync();
+        hsd_free(g_scr[d][cls]);
+        g_scr[d][cls] = hsd_malloc(bytes);
+        g_scr_sz[d][cls] = g_scr[d][cls] ? bytes : 0;
+    }
+    return g_scr[d][cls];
+}
+
+static size_t chunk_bytes(void)
+{
+    static size_t v = 0;
+    if (!v) {
+        const char *s = getenv("HSFFT_CHUNK_MB");
+        v = (size_t)(s ? atof(s) : 256.0) * (1u << 20);
+        if (v < (1u << 20)) v = 1u << 20;
+    }
+    return v;
+}
+
+/* ------------------------------------------------------------------ device state */
+static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idist, void *O, long long odist,
+                     int batch, int sgn, int conj, int dir, int load_op, const void *laux, int store_op,
+                     const void *saux, long long nsig);
+
+static hs_devstate *devstate(hs_entry *e)
+{
+    const int d = hsd_get_device();
+    if (d < 0 || d >= HS_MAX_DEV) {
+        hs_seterr("invalid current device %d", d);
+        return NULL;
+    }
+    if (e->ds[d] && e->ds_version[d] == e->version) return e->ds[d];
+    free_devstate(e->ds[d]);
+    e->ds[d] = NULL;
+    hs_devstate *s = calloc(1, sizeof *s);
+    const size_t twb = sizeof(fft_data) * (size_t)(e->M > 1 ? e->M : 1);
+    const fft_data *twsrc = e->tw_from_struct ? e->key->twiddle : e->tw_private;
+    s->d_tw = hsd_malloc(twb);
+    if (!s->d_tw || hsd_h2d(s->d_tw, twsrc, sizeof(fft_data) * (size_t)(e->M > 1 ? e->M - 1 : 0))) goto fail;
+    if (e->ngcs) {
+        s->d_gcs = hsd_malloc(sizeof(double) * (size_t)e->ngcs);
+        if (!s->d_gcs || hsd_h2d(s->d_gcs, e->gcs, sizeof(double) * (size_t)e->ngcs)) goto fail;
+    }
+    if (e->lt == 1) {
+        const int N = e->N, M = e->M;
+        s->d_chirp = hsd_malloc(sizeof(fft_data) * (size_t)N);
+        s->d_hk = hsd_malloc(sizeof(fft_data) * (size_t)M);
+        if (!s->d_chirp || !s->d_hk || hsd_h2d(s->d_chirp, e->chirp, sizeof(fft_data) * (size_t)N)) goto fail;
+        /* hk = FFT_M(hl / M): padded + mirrored chirp (ref :1692-1703), scaled (:1787-1792),
+         * transformed with the plan's own sign and twiddles (:1797) -- once per plan */
+        fft_data *hl = calloc((size_t)M, sizeof(fft_data));
+        const double scale = 1.0 / M;
+        for (int i = 0; i < M; i++) {
+            fft_data v = {0.0, 0.0};
+            if (i < N) v = e->chirp[i];
+            else if (i >= M - N + 1) v = e->chirp[M - i];
+            hl[i].im = v.im * scale;
+            hl[i].re = v.re * scale;
+        }
+        void *d_hl = hsd_malloc(sizeof(fft_data) * (size_t)M);
+        int rc = d_hl ? hsd_h2d(d_hl, hl, sizeof(fft_data) * (size_t)M) : -1;
+        free(hl);
+        e->ds[d] = s; /* run_chain needs the twiddles */
+        if (!rc) rc = run_chain(e, s, d_hl, M, s->d_hk, M, 1, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL,
+                                HS_STORE_PLAIN, NULL, M);
+        if (!rc) rc = hsd_sync();
+        hsd_free(d_hl);
+        e->ds[d] = NULL;
+        if (rc) goto fail;
+    }
+    e->ds[d] = s;
+    e->ds_version[d] = e->version;
+    return s;
+fail:
+    if (!g_errbuf[0]) hs_seterr("device state: %s", hsd_errstr());
+    free_devstate(s);
+    return NULL;
+}
+
+/* ------------------------------------------------------------------ pass chains */
+static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long long idist, void *out,
+                       long long odist, int batch, int sgn, int conj, int dir, int load_op, const void *laux,
+                       int store_op, const void *saux, long long nsig)
+{
+    hsd_launch l;
+    memset(&l, 0, sizeof l);
+    l.in = in;
+    l.out = out;
+    l.idist = idist;
+    l.odist = odist;
+    l.batch = batch;
+    l.sgn = sgn;
+    l.dir = dir;
+    l.conj = conj;
+    l.tw = ds->d_tw;
+    l.gcs = (const double *)ds->d_gcs;
+    l.load_op = load_op;
+    l.load_aux = laux;
+    l.store_op = store_op;
+    l.store_aux = saux;
+    l.nsig = nsig;
+    int rc = hsd_run_pass(&e->pass[i], &l);
+    if (rc) hs_seterr("pass %d: %s", i, hsd_errstr());
+    return rc;
+}
+
+/* One mixed-radix transform of length M per row, chained over the plan's passes.  Reads
+ * I (never written), writes O.  Intermediate buffers come from the scratch pool; the last
+ * pass (A == 1: it reads and writes the same element set per tile) may run in place on O
+ * when O is a plain M-length row buffer. */
+static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idist, void *O, long long odist,
+                     int batch, int sgn, int conj, int dir, int load_op, const void *laux, int store_op,
+                     const void *saux, long long nsig)
+{
+    const int n = e->npass;
+    const long long M = e->M;
+    if (M == 1 || n == 0) { /* N == 1: the reference copies (ref :332-342) */
+        for (int b = 0; b < batch; b++)
+            if (hsd_d2d_async((fft_data *)O + b * odist, (const fft_data *)I + b * idist, sizeof(fft_data))) return -2;
+        return 0;
+    }
+    if (n == 1)
+        return launch_pass(e, ds, 0, I, idist, O, odist, batch, sgn, conj, dir, load_op, laux, store_op, saux, nsig);
+    const int last_inplace = store_op != HS_STORE_CHIRP && odist == M;
+    /* passes 0..n-2 write scratch except that pass n-2 writes O when the last pass can run
+     * in place; consecutive scratch writes alternate between two buffers */
+    const int writes = (n - 1) - (last_inplace ? 1 : 0);
+    const int need = writes < 2 ? writes : 2;
+    long long chunk = batch;
+    if (need) {
+        long long per = (long long)(chunk_bytes() / (sizeof(fft_data) * (size_t)M));
+        if (per < 1) per = 1;
+        if (chunk > per) chunk = per;
+    }
+    void *S[2] = {NULL, NULL};
+    for (int k = 0; k < need; k++) {
+        S[k] = hs_scratch(k, sizeof(fft_data) * (size_t)(chunk * M));
+        if (!S[k]) {
+            hs_seterr("scratch allocation of %lld bytes failed", (long long)(chunk * M * 16));
+            return HSFFT_ERR_NOMEM;
+        }
+    }
+    for (long long c0 = 0; c0 < batch; c0 += chunk) {
+        const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
+        const void *R = (const fft_data *)I + c0 * idist;
+        long long rdist = idist;
+        int lop = load_op, j = 0;
+        for (int i = 0; i < n; i++) {
+            void *W;
+            long long wdist;
+            if (i == n - 1 || (i == n - 2 && last_inplace)) {
+                W = (fft_data *)O + c0 * odist;
+                wdist = odist;
+            } else {
+                W = S[j++ & 1];
+                wdist = M;
+            }
+            const int sop = i == n - 1 ? store_op : HS_STORE_PLAIN;
+            int rc = launch_pass(e, ds, i, R, rdist, W, wdist, cb, sgn, conj, dir, lop, laux, sop, saux, nsig);
+            if (rc) return rc;
+            R = W;
+            rdist = wdist;
+            lop = HS_LOAD_PLAIN;
+        }
+    }
+    return 0;
+}
+
+/* Bluestein (ref :1735-1907) on rows of length N: pre-multiply fused into the first pass of
+ * FFT #2, the spectrum product into its last pass, FFT #3 runs with conjugated twiddles and
+ * sign -sgn, the post-multiply is fused into its last pass.  hk was computed once per plan. */
+static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long idist, void *out, long long odist,
+                         int batch)
+{
+    const long long M = e->M, N = e->N;
+    long long chunk = (long long)(chunk_bytes() / (sizeof(fft_data) * (size_t)M));
+    if (chunk < 1) chunk = 1;
+    if (chunk > batch) chunk = batch;
+    void *mid = hs_scratch(3, sizeof(fft_data) * (size_t)(chunk * M));
+    if (!mid) return HSFFT_ERR_NOMEM;
+    for (long long c0 = 0; c0 < batch; c0 += chunk) {
+        const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
+        int rc = run_chain(e, ds, (const fft_data *)in + c0 * idist, idist, mid, M, cb, e->sgn, 0, e->sgn,
+                           HS_LOAD_CHIRP, ds->d_chirp, HS_STORE_SPEC, ds->d_hk, N);
+        if (!rc)
+            rc = run_chain(e, ds, mid, M, (fft_data *)out + c0 * odist, odist, cb, -1 * e->sgn, 1, e->sgn,
+                           HS_LOAD_PLAIN, NULL, HS_STORE_CHIRP, ds->d_chirp, N);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long long odist, int batch)
+{
+    hs_devstate *ds = devstate(e);
+    if (!ds) return HSFFT_ERR_DEVICE;
+    if (e->lt == 1) return run_bluestein(e, ds, in, idist, out, odist, batch);
+    return run_chain(e, ds, in, idist, out, odist, batch, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN,
+                     NULL, e->M);
+}
+
+/* ------------------------------------------------------------------ drop-in fft_exec */
+void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
+{
+    if (obj == NULL || inp == NULL || oup == NULL) {
+        fprintf(stderr, "Error: Invalid FFT object or data pointers\n");
+        exit(EXIT_FAILURE);
+    }
+    if (obj->lt != 0 && obj->lt != 1) {
+        fprintf(stderr, "Error: Invalid FFT object type (lt = %d)\n", obj->lt);
+        exit(EXIT_FAILURE);
+    }
+    g_errbuf[0] = 0;
+    if (hs_require_gpu()) fatal("fft_exec needs an MI355X");
+    hs_entry *e = hs_entry_get(obj);
+    if (!e) fatal("fft_exec: invalid plan");
+    const int N = obj->N;
+    const size_t bytes = sizeof(fft_data) * (size_t)N;
+    const int din = hsd_is_device_ptr(inp), dout = hsd_is_device_ptr(oup);
+    int rc;
+    if (din && dout && inp != oup) {
+        rc = hs_c2c_rows(e, inp, N, oup, N, 1);
+    } else {
+        /* host (or aliased) buffers: staged through device memory, synchronous */
+        fft_data *di = hs_scratch(5, bytes), *dq = hs_scratch(6, bytes);
+        if (!di || !dq) fatal("fft_exec: device staging allocation failed");
+        rc = din ? hsd_d2d_async(di, inp, bytes) : hsd_h2d(di, inp, bytes);
+        if (!rc) rc = hs_c2c_rows(e, di, N, dq, N, 1);
+        if (!rc) rc = dout ? hsd_d2d_async(oup, dq, bytes) : hsd_d2h(oup, dq, bytes);
+    }
+    if (!rc) rc = hsd_sync();
+    if (rc) fatal("fft_exec failed");
+}
+
+/* ------------------------------------------------------------------ extension API */
+int hsfft_device_count(void) { return hsd_device_count(); }
+int hsfft_set_device(int dev) { return hsd_set_device(dev) ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_get_device(void) { return hsd_get_device(); }
+void *hsfft_malloc(size_t bytes) { return hs_require_gpu() ? NULL : hsd_malloc(bytes); }
+int hsfft_free(void *p) { return hsd_free(p) ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_memcpy_h2d(void *d, const void *h, size_t n) { return hsd_h2d(d, h, n) ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_memcpy_d2h(void *h, const void *d, size_t n) { return hsd_d2h(h, d, n) ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_memset(void *d, int v, size_t n) { return hsd_memset_async(d, v, n) ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_synchronize(void) { return hsd_sync() ? HSFFT_ERR_DEVICE : 0; }
+void *hsfft_get_stream(void) { return hsd_stream(); }
+
+int hsfft_plan_refresh(fft_object obj)
+{
+    if (!obj) return HSFFT_ERR_ARG;
+    hs_entry *e = hs_entry_get(obj);
+    if (!e) return HSFFT_ERR_ARG;
+    e->version++;
+    return 0;
+}
+
+int hsfft_plan_num_passes(fft_object obj)
+{
+    if (!obj) return HSFFT_ERR_ARG;
+    hs_entry *e = hs_entry_get(obj);
+    return e ? e->npass : HSFFT_ERR_ARG;
+}
+
+static int drmap(const struct fft_set *o, int *map, int oo, int io, int stride, int n, int fi)
+{
+    if (n == 1 || is_leaf_len(n)) { /* leaf gather: out slot oo+i <- in index io+i*stride */
+        for (int i = 0; i < n; i++) map[oo + i] = io + i * stride;
+        return 0;
+    }
+    if (fi >= o->lf || o->factors[fi] <= 1 || n % o->factors[fi]) return HSFFT_ERR_ARG;
+    const int r = o->factors[fi], L = n / r;
+    for (int i = 0; i < r; i++)
+        if (drmap(o, map, oo + i * L, io + i * stride, stride * r, L, fi + 1)) return HSFFT_ERR_ARG;
+    return 0;
+}
+
+int hsfft_digit_reverse_map(fft_object obj, int *map)
+{
+    if (!obj || !map || obj->lt != 0 || obj->N < 1) return HSFFT_ERR_ARG;
+    return drmap(obj, map, 0, 0, 1, obj->N, 0);
+}
+
+int hsfft_exec_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch)
+{
+    g_errbuf[0] = 0;
+    if (!obj || !d_in || !d_out || batch < 0 || d_in == d_out) {
+        hs_seterr("hsfft_exec_batched: invalid arguments");
+        return HSFFT_ERR_ARG;
+    }
+    if (batch == 0) return 0;
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    hs_entry *e = hs_entry_get(obj);
+    if (!e) return HSFFT_ERR_ARG;
+    return hs_c2c_rows(e, d_in, obj->N, d_out, obj->N, batch);
+}
+
+int hsfft_fill_complex(fft_data *d_x, int64_t count, uint64_t seed, uint64_t offset)
+{
+    int rc = hs_require_gpu();
+    return rc ? rc : (hsd_fill_complex(d_x, count, seed, offset) ? HSFFT_ERR_DEVICE : 0);
+}
+
+int hsfft_fill_real(fft_type *d_x, int64_t count, uint64_t seed, uint64_t offset)
+{
+    int rc = hs_require_gpu();
+    return rc ? rc : (hsd_fill_real(d_x, count, seed, offset) ? HSFFT_ERR_DEVICE : 0);
+}
+
+int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch, int iters, float *ms,
+                       float *pass_ms, int max_pass)
+{
+    if (!obj || iters < 1 || !ms) return HSFFT_ERR_ARG;
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    hs_entry *e = hs_entry_get(obj);
+    if (!e) return HSFFT_ERR_ARG;
+    if (hsd_timer_start()) return HSFFT_ERR_DEVICE;
+    for (int it = 0; it < iters; it++) {
+        rc = hs_c2c_rows(e, d_in, obj->N, d_out, obj->N, batch);
+        if (rc) return rc;
+    }
+    if (hsd_timer_stop(ms)) return HSFFT_ERR_DEVICE;
+    if (pass_ms && max_pass > 0 && e->lt == 0 && e->npass > 0) {
+        /* one instrumented iteration: events around every pass launch of a 2-pass in-place
+         * chain (the chain's own launch order), so per-kernel averages can be reported */
+        hs_devstate *ds = devstate(e);
+        const int n = e->npass < max_pass ? e->npass : max_pass;
+        if (e->npass <= 2 && ds) {
+            for (int i = 0; i < e->npass; i++) {
+                const void *R = i == 0 ? (const void *)d_in : (const void *)d_out;
+                if (i < n) hsd_pass_timer_begin(i);
+                rc = launch_pass(e, ds, i, R, obj->N, d_out, obj->N, batch, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL,
+                                 HS_STORE_PLAIN, NULL, e->M);
+                if (i < n) hsd_pass_timer_end(i);
+                if (rc) return rc;
+            }
+            hsd_pass_timer_read(n, pass_ms);
+        } else {
+            for (int i = 0; i < n; i++) pass_ms[i] = -1.0f;
+        }
+    }
+    return 0;
+}
+
+int hsfft_exec_multi(fft_object obj, const fft_data *const *d_in, fft_data *const *d_out, int batch, int ndev)
+{
+    if (!obj || !d_in || !d_out || ndev < 1 || batch < 0) return HSFFT_ERR_ARG;
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    if (ndev > hsd_device_count()) return HSFFT_ERR_ARG;
+    const int cur = hsd_get_device();
+    /* launches are asynchronous per device stream, so one host thread can keep every
+     * device busy; each device gets its contiguous shard, no data crosses devices */
+    for (int g = 0; g < ndev && !rc; g++) {
+        const int b0 = (int)((long long)batch * g / ndev), b1 = (int)((long long)batch * (g + 1) / ndev);
+        if (hsd_set_device(g)) return HSFFT_ERR_DEVICE;
+        rc = hsfft_exec_batched(obj, d_in[g], d_out[g], b1 - b0);
+    }
+    for (int g = 0; g < ndev; g++) {
+        hsd_set_device(g);
+        if (hsd_sync()) rc = rc ? rc : HSFFT_ERR_DEVICE;
+    }
+    if (cur >= 0) hsd_set_device(cur);
+    return rc;
+}

@@ -1,0 +1,64 @@
+/*
+ * hsfft_host.h -- host-side internals shared by the C translation units of libhsfft.so.
+ */
+#ifndef HSFFT_HOST_H_
+#define HSFFT_HOST_H_
+
+#include "highspeedFFT.h"
+#include "hsfft_internal.h"
+#include "real.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-device state of one plan: device copies of what the plan needs */
+typedef struct hs_devstate {
+    void *d_tw;   /* M-1 (+1) complex twiddles, copied from the public struct */
+    void *d_gcs;  /* odd-radix cos/sin constants */
+    void *d_chirp;/* Bluestein chirp h(n), N complex */
+    void *d_hk;   /* Bluestein spectrum of the scaled, mirrored chirp, M complex */
+} hs_devstate;
+
+/* schedule derived from the public plan fields (snapshot) */
+typedef struct hs_entry {
+    const struct fft_set *key;
+    int N, sgn, lt, lf, M; /* M = length of the mixed-radix transform actually run */
+    int factors[64];       /* snapshot of the public fields (edits trigger a rebuild) */
+    int rlf, rfac[64];     /* factor list actually executed (differs only for D5) */
+    int tw_from_struct;    /* 1: twiddles copied from the struct; 0: private table (D5) */
+    fft_data *tw_private;  /* Bluestein plan/exec length mismatch (D5): own M_exec table */
+    int nst;
+    int stage_r[HS_MAX_STAGES];  /* innermost first */
+    int first_leaf;
+    int npass;
+    hsd_pass pass[HS_MAX_PASSES];
+    double *gcs;           /* host odd-radix constants */
+    int ngcs;
+    fft_data *chirp;       /* Bluestein chirp (host) */
+    hs_devstate *ds[HS_MAX_DEV];
+    int version;           /* bumped by hsfft_plan_refresh: device copies re-uploaded */
+    int ds_version[HS_MAX_DEV];
+    struct hs_entry *next;
+} hs_entry;
+
+/* planner (hsfft_plan.c) */
+int hs_twiddle_mode(void);
+void hs_longvector(fft_data *tw, int M, const int *fac, int lf, int exact);
+int hs_bluestein_M_init(int N); /* fft_init sizing (log10), ref :242-252 */
+int hs_bluestein_M_exec(int N); /* bluestein_fft sizing (log2), ref :1750-1751 */
+
+/* registry / scheduling / execution (hsfft_exec.c) */
+hs_entry *hs_entry_get(const struct fft_set *obj);
+void hs_entry_release(const struct fft_set *obj);
+int hs_require_gpu(void);
+void hs_seterr(const char *fmt, ...);
+int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long long odist, int batch);
+/* scratch buffers per device: class 0..2 chain pool, 3 Bluestein mid, 4 real staging, 5-7 misc */
+void *hs_scratch(int cls, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,105 @@
+/*
+ * hsfft_internal.h -- internal interface between the C host side (planner, drop-in API,
+ * scheduler) and the HIP/CDNA4 device layer (hsfft_device.hip).  Not installed.
+ *
+ * Execution model: the reference recursion is replaced by a
+ * Stockham autosort schedule.  Stage s (innermost first) has radix r_s and global
+ * L_s = r_0...r_{s-1}; after it, sub-transform m (of length L_s*r_s) sits at
+ * [m*L_s*r_s, (m+1)*L_s*r_s).  Consecutive stages are fused into passes; a pass of P points
+ * with L0 = B at its start views its input as [t][m][q] (P x A x B, A = M/(B*P)) and writes
+ * [m][u][q]: a P-point sub-FFT along t for every (m, q), using the plan's global twiddles
+ * tw[L-1 + (r-1)*k + i-1] with k = q + B*k_local.
+ */
+#ifndef HSFFT_INTERNAL_H_
+#define HSFFT_INTERNAL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HS_MAX_STAGES 64
+#define HS_MAX_PASS_STAGES 12
+#define HS_MAX_PASSES 16
+#define HS_MAX_DEV 16
+
+/* kernel variants */
+#define HS_KV_GENERIC 0   /* runtime radix list, LDS ping-pong */
+#define HS_KV_R8X3 1      /* specialised: 8*8*8 or tails, register butterflies */
+
+/* load / store hooks of a pass (Bluestein fusion) */
+#define HS_LOAD_PLAIN 0
+#define HS_LOAD_CHIRP 1   /* x[n]*conj-chirp for n < nsig, 0 for n >= nsig (:1803-1827) */
+#define HS_STORE_PLAIN 0
+#define HS_STORE_SPEC 1   /* y[n]*hk[n] (:1838-1855) */
+#define HS_STORE_CHIRP 2  /* y[n]*chirp for n < nsig only (:1871-1886) */
+
+typedef struct {
+    int nst;                        /* stages fused in this pass */
+    int radix[HS_MAX_PASS_STAGES];  /* innermost first */
+    int gcs_off[HS_MAX_PASS_STAGES];/* generic-radix constant offsets (doubles) or -1 */
+    int P;                          /* points per group */
+    int leaf;                       /* first stage is the reference leaf (global L == 1) */
+    long long B;                    /* L at pass start */
+    long long A;                    /* M / (B*P) */
+    int Wm, Wq, G;                  /* tile: Wm m-values x Wq q-values, G = Wm*Wq groups */
+    int variant;                    /* HS_KV_* */
+} hsd_pass;
+
+typedef struct {
+    const void *in;
+    void *out;
+    long long idist, odist;         /* batch strides in complex elements */
+    int batch;
+    int sgn;                        /* butterfly sign of this transform */
+    int dir;                        /* Bluestein transform_direction for the hooks */
+    int conj;                       /* negate twiddle imaginary parts */
+    const void *tw;
+    const double *gcs;
+    int load_op, store_op;
+    const void *load_aux, *store_aux;
+    long long nsig;
+} hsd_launch;
+
+/* device layer (hsfft_device.hip) */
+int hsd_device_count(void);
+int hsd_set_device(int dev);
+int hsd_get_device(void);
+void *hsd_malloc(size_t bytes);
+int hsd_free(void *p);
+int hsd_h2d(void *d, const void *h, size_t bytes);
+int hsd_d2h(void *h, const void *d, size_t bytes);
+int hsd_d2d_async(void *d, const void *s, size_t bytes);
+int hsd_memset_async(void *d, int v, size_t bytes);
+int hsd_sync(void);
+void *hsd_stream(void);
+int hsd_is_device_ptr(const void *p);
+const char *hsd_errstr(void);
+
+int hsd_run_pass(const hsd_pass *p, const hsd_launch *l);
+int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset);
+int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset);
+/* r2c split (real.c:108-132): Z rows of h complex -> X rows of 2h complex */
+int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist);
+/* c2r pre-twiddle (real.c:169-179): X rows (>= h+1 complex) -> Zin rows of h complex */
+int hsd_c2r_pre(const void *X, const void *tw2, void *Zin, int h, int batch, long long xdist, long long zdist);
+/* convolution helpers (convolve.c:147-160) */
+int hsd_cmul(const void *A, const void *Bv, void *C, long long n, int batch, long long dist);
+int hsd_scale_real(void *x, long long n, int batch, long long dist, double divisor);
+int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
+                  long long dlen, int batch);
+
+/* timing on the library stream */
+int hsd_timer_start(void);
+int hsd_timer_stop(float *ms);
+int hsd_pass_timer_begin(int i);
+int hsd_pass_timer_end(int i);
+int hsd_pass_timer_read(int n, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

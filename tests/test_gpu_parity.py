@@ -1,0 +1,302 @@
+"""GPU parity: libhsfft on the MI355X against the oracle (CPU restatement pinned to the
+reference) and the golden fixtures generated from the reference itself.
+
+Tolerance: BIT-EXACT (0 ulp) for every comparison against the oracle / fixtures -- the GPU
+path keeps the reference's twiddle tables, operand order and separate roundings.  The only
+non-bit-exact checks are against numpy (independent truth), at 4*eps*max|X| for the
+full-precision radix-2/4/8 sizes and 1e-10 relative where the reference's 11-digit radix-3/5/7
+constants limit accuracy.
+
+Reference defects and the policy here: D1 (radix-2 leaf reads its
+stale output slot) is NOT reproduced -- D1 sizes compare against the reference's "fixed"
+flavour; D2 (twiddle-table quirk) IS reproduced in the default twiddle mode; D3 (radix 13),
+D5 (N=2^k+1 Bluestein) and D6 (N=1) compute the correct transform where the reference crashes
+or reads out of bounds.
+"""
+import numpy as np
+import pytest
+
+import hsfft_testlib as T
+
+import hsfft
+
+pytestmark = pytest.mark.gpu
+
+EPS = np.finfo(np.float64).eps
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if hsfft.device_count() < 1:
+        pytest.skip("no GPU")
+    hsfft.lib().hsfft_set_device(0)
+    yield
+    hsfft.synchronize()
+
+
+def gpu_c2c_batched(n, sgn, x):
+    """device-resident batched path"""
+    x = np.ascontiguousarray(x, dtype=np.complex128)
+    batch = x.shape[0] if x.ndim == 2 else 1
+    p = hsfft.Plan(n, sgn)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    hsfft.exec_batched(p, din, dout, batch)
+    hsfft.synchronize()
+    y = dout.to_array(np.complex128).reshape(x.shape)
+    din.free()
+    dout.free()
+    p.close()
+    return y
+
+
+def oracle_rows(x, sgn, flags=0):
+    return T.oracle_c2c(x, sgn, flags)
+
+
+# every golden c2c size; D1 sizes are compared against the fixed flavour (oracle flags 0)
+C2C_SIZES = [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 19, 20, 22, 25, 27, 32, 36, 45, 49, 60, 64,
+             97, 100, 121, 125, 128, 243, 256, 343, 512, 1021, 1024, 4096, 5003, 12600, 65536]
+
+
+@pytest.mark.parametrize("n", C2C_SIZES)
+def test_c2c_dropin_host_pointers_bit_exact(n):
+    """fft_exec with host buffers (the reference's own calling convention)."""
+    for sgn in (1, -1):
+        x = T.complex_input(n, T.seed_for(n))
+        y = hsfft.Plan(n, sgn).exec(x)
+        assert T.bits_equal(y, oracle_rows(x, sgn)), (n, sgn, T.mismatches(y, oracle_rows(x, sgn)))
+
+
+@pytest.mark.parametrize("n", C2C_SIZES)
+def test_c2c_batched_device_bit_exact(n):
+    rows = 3 if n <= 65536 else 1
+    for sgn in (1, -1):
+        x = T.complex_input(n, T.seed_for(n) ^ 0x77, batch=rows).reshape(rows, n)
+        y = gpu_c2c_batched(n, sgn, x)
+        assert T.bits_equal(y, oracle_rows(x, sgn)), (n, sgn)
+
+
+def test_c2c_matches_reference_fixtures(golden):
+    """Golden outputs of the reference itself.  'asis' cases whose factor list ends in 2 are
+    D1-affected (their output depends on the caller's buffer) and are covered by the 'fixed'
+    flavour, which is compared in exact-twiddle mode."""
+    meta, data = golden
+    checked = 0
+    for key, ent in sorted(meta["cases"].items()):
+        if ent.get("kind") != "c2c" or not ent.get("full", False):
+            continue
+        n, sgn = ent["n"], ent["sgn"]
+        if ent["flavour"] == "asis" and ent["plan"]["factors"][-1:] == [2]:
+            continue
+        hsfft.set_twiddle_mode("exact" if ent["flavour"] == "fixed" else "reference")
+        try:
+            y = hsfft.Plan(n, sgn).exec(T.complex_input(n, ent["seed"]))
+        finally:
+            hsfft.set_twiddle_mode("reference")
+        assert T.bits_equal(y, data[key]), (key, T.mismatches(y, data[key]))
+        checked += 1
+    assert checked >= 60
+
+
+def test_config1_n1024_fixed_flavour(golden):
+    """BASELINE config 1 (N=1024, single transform): the reference's radix-2 leaf reads its
+    stale output slot (D1); with that neutralised its output is exactly ours."""
+    meta, data = golden
+    x = T.complex_input(1024, T.SEEDS[1])
+    hsfft.set_twiddle_mode("exact")  # 1024 = [8,8,8,2]: exact == reference twiddles here
+    try:
+        y = hsfft.Plan(1024, 1).exec(x)
+    finally:
+        hsfft.set_twiddle_mode("reference")
+    assert T.bits_equal(y, data["c2c_fixed_1024_p"])
+    y2 = hsfft.Plan(1024, 1).exec(x)
+    assert T.bits_equal(y2, data["c2c_fixed_1024_p"])
+    X = np.fft.fft(x)
+    assert np.abs(y - X).max() <= 4 * EPS * np.abs(X).max()
+
+
+def test_config2_2pow20_rows_and_fixture(golden):
+    meta, data = golden
+    n = 1 << 20
+    x = T.complex_input(n, T.SEEDS[2], batch=2).reshape(2, n)
+    y = gpu_c2c_batched(n, 1, x)
+    assert T.bits_equal(y, oracle_rows(x, 1))
+    key = "c2c_asis_1048576_p"
+    assert T.bits_equal(y[0][data[key + "__idx"]], data[key + "__val"])
+    assert T.sha256(y[0]) == meta["cases"][key]["sha256"]
+    X = np.fft.fft(x[1])
+    assert np.abs(y[1] - X).max() <= 4 * EPS * np.abs(X).max()
+
+
+def test_config3_12600_reference_mode_and_exact_mode(golden):
+    meta, data = golden
+    n = 12600
+    x = T.complex_input(n, T.SEEDS[3], batch=16).reshape(16, n)
+    y = gpu_c2c_batched(n, 1, x)
+    assert T.bits_equal(y, oracle_rows(x, 1))  # reference mode reproduces the D2 quirk
+    assert T.bits_equal(y[0], data["c2c_asis_12600_p"])
+    hsfft.set_twiddle_mode("exact")
+    try:
+        ye = gpu_c2c_batched(n, 1, x)
+    finally:
+        hsfft.set_twiddle_mode("reference")
+    assert T.bits_equal(ye, oracle_rows(x, 1, T.ORC_EXACT))
+    assert T.bits_equal(ye[0], data["c2c_fixed_12600_p"])
+    X = np.fft.fft(x, axis=1)
+    assert np.abs(ye - X).max() / np.abs(X).max() < 1e-10  # 11-digit radix-3/5/7 constants
+
+
+def test_config4_bluestein_99991(golden):
+    meta, data = golden
+    n = 99991
+    for sgn in (1, -1):
+        x = T.complex_input(n, T.SEEDS[4], batch=3).reshape(3, n)
+        y = gpu_c2c_batched(n, sgn, x)
+        assert T.bits_equal(y, oracle_rows(x, sgn)), sgn
+        key = f"c2c_asis_99991_{'p' if sgn == 1 else 'm'}"
+        assert T.bits_equal(y[0][data[key + "__idx"]], data[key + "__val"])
+        assert T.sha256(y[0]) == meta["cases"][key]["sha256"]
+    X = np.fft.fft(x[0])
+    y = gpu_c2c_batched(n, 1, x[:1])[0]
+    assert np.abs(y - X).max() <= 8 * EPS * np.abs(X).max()
+
+
+def test_config5_r2c_2pow22(golden):
+    meta, data = golden
+    n = 1 << 22
+    x = T.real_input(n, T.SEEDS[5], batch=2).reshape(2, n)
+    rp = hsfft.RealPlan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(2 * n * 16)
+    hsfft.r2c_batched(rp, din, dout, 2)
+    y = dout.to_array(np.complex128).reshape(2, n)
+    ref = T.oracle_r2c(x, 1)
+    assert T.bits_equal(y, ref)
+    key = "r2c_4194304_p"
+    assert T.bits_equal(y[0][data[key + "__idx"]], data[key + "__val"])
+    assert T.sha256(y[0]) == meta["cases"][key]["sha256"]
+
+
+def test_real_small_fixtures(golden):
+    meta, data = golden
+    for key, ent in sorted(meta["cases"].items()):
+        if ent.get("kind") == "r2c" and ent["full"]:
+            x = T.real_input(ent["n"], ent["seed"])
+            y = hsfft.RealPlan(ent["n"], ent["sgn"]).r2c(x)
+            assert T.bits_equal(y, data[key]), key
+        if ent.get("kind") == "c2r":
+            y = hsfft.RealPlan(ent["n"], ent["sgn"]).c2r(data[ent["input_key"]])
+            assert T.bits_equal(y, data[key]), key
+
+
+def test_c2r_batched_matches_oracle():
+    n = 1 << 16
+    X = T.oracle_r2c(T.real_input(n, 11, batch=3).reshape(3, n), 1)
+    rp = hsfft.RealPlan(n, -1)
+    din = hsfft.DeviceBuffer.from_array(X)
+    dout = hsfft.DeviceBuffer(3 * n * 8)
+    hsfft.c2r_batched(rp, din, dout, 3)
+    y = dout.to_array(np.float64).reshape(3, n)
+    for b in range(3):
+        assert T.bits_equal(y[b], T.oracle_c2r(X[b], n, -1))
+
+
+def test_convolve_fixtures(golden):
+    meta, data = golden
+    L = hsfft.lib()
+    for key, ent in sorted(meta["cases"].items()):
+        if ent.get("kind") != "conv":
+            continue
+        a = T.real_input(ent["n"], ent["seed_a"])
+        b = T.real_input(ent["m"], ent["seed_b"])
+        o = np.zeros(4 * (ent["n"] + ent["m"]))
+        ln = L.fft_convolve(ent["type"].encode(), ent["conv_type"].encode(), T.ptr(a), ent["n"], T.ptr(b), ent["m"],
+                            T.ptr(o))
+        assert ln == ent["len"], key
+        assert T.bits_equal(o[:ln], data[key]), key
+
+
+def test_convolve_batched_matches_oracle():
+    L = hsfft.lib()
+    n, m, rows = 300, 17, 4
+    a = T.real_input(n, 5, batch=rows).reshape(rows, n)
+    b = T.real_input(m, 6, batch=rows).reshape(rows, m)
+    da, db = hsfft.DeviceBuffer.from_array(a), hsfft.DeviceBuffer.from_array(b)
+    for typ in (b"full", b"same", b"valid"):
+        dout = hsfft.DeviceBuffer(rows * (n + m) * 8)
+        ln = L.hsfft_convolve_batched(typ, b"linear", da.ptr, n, db.ptr, m, dout.ptr, rows)
+        assert ln > 0
+        y = dout.to_array(np.float64, rows * ln).reshape(rows, ln)
+        lib = T.oracle()
+        for r in range(rows):
+            o = np.zeros(2 * (n + m))
+            assert lib.orc_convolve(typ, b"linear", T.ptr(np.ascontiguousarray(a[r])), n,
+                                    T.ptr(np.ascontiguousarray(b[r])), m, T.ptr(o), 0) == ln
+            assert T.bits_equal(y[r], o[:ln]), (typ, r)
+
+
+def test_divergences_d3_d5_d6():
+    """radix 13 (reference segfaults, D3), N=2^k+1 Bluestein (reference reads past its
+    twiddles, D5), N=1 (reference exits, D6): correct results here, bit-exact vs oracle."""
+    for n in [13, 26, 169, 257, 1025, 1]:
+        for sgn in (1, -1):
+            x = T.complex_input(n, T.seed_for(n))
+            y = hsfft.Plan(n, sgn).exec(x)
+            assert T.bits_equal(y, oracle_rows(x, sgn)), (n, sgn)
+            X = np.fft.fft(x) if sgn == 1 else np.fft.ifft(x) * n
+            assert np.abs(y - X).max() <= 1e-12 * max(1.0, np.abs(X).max()), n
+
+
+def test_generic_odd_radices():
+    for n in [11, 121, 17 * 8, 23 * 4, 29 * 3, 31, 37 * 5, 41, 43 * 2, 47, 53 * 8]:
+        x = T.complex_input(n, 3, batch=2).reshape(2, n)
+        for sgn in (1, -1):
+            assert T.bits_equal(gpu_c2c_batched(n, sgn, x), oracle_rows(x, sgn)), (n, sgn)
+
+
+def test_batch_edge_cases():
+    L = hsfft.lib()
+    p = hsfft.Plan(64, 1)
+    d = hsfft.DeviceBuffer(64 * 16)
+    assert L.hsfft_exec_batched(p.ptr, d.ptr, d.ptr, 1) < 0      # in == out refused
+    assert L.hsfft_exec_batched(p.ptr, d.ptr, hsfft.DeviceBuffer(16).ptr, 0) == 0  # empty batch
+    assert L.hsfft_exec_batched(None, d.ptr, d.ptr, 1) < 0
+
+
+def test_full_size_config2_properties():
+    """BASELINE config 2 at full size (4096 x 2^20, 64 GiB in / 64 GiB out): sampled rows
+    bit-exact vs the oracle and a forward/inverse round trip."""
+    n, batch = 1 << 20, 4096
+    p, pi = hsfft.Plan(n, 1), hsfft.Plan(n, -1)
+    din = hsfft.DeviceBuffer(batch * n * 16)
+    dout = hsfft.DeviceBuffer(batch * n * 16)
+    hsfft.fill_complex(din, batch * n, T.SEEDS[2])
+    hsfft.exec_batched(p, din, dout, batch)
+    hsfft.synchronize()
+    for row in (0, 1777, batch - 1):
+        y = dout.to_array(np.complex128, n, row * n * 16)
+        x = T.complex_input(n, T.SEEDS[2], batch=1, row0=row)
+        assert T.bits_equal(y, oracle_rows(x, 1)), row
+    # inverse of the first 8 rows back into din's head: round trip
+    hsfft.exec_batched(pi, dout, din, 8)
+    hsfft.synchronize()
+    z = din.to_array(np.complex128, 8 * n).reshape(8, n) / n
+    x = T.complex_input(n, T.SEEDS[2], batch=8).reshape(8, n)
+    assert np.abs(z - x).max() < 1e-13
+    din.free()
+    dout.free()
+
+
+def test_multi_device_api_single_gpu():
+    L = hsfft.lib()
+    n, batch = 4096, 8
+    p = hsfft.Plan(n, 1)
+    x = T.complex_input(n, 9, batch=batch).reshape(batch, n)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    import ctypes
+    ins = (ctypes.c_void_p * 1)(din.ptr)
+    outs = (ctypes.c_void_p * 1)(dout.ptr)
+    assert L.hsfft_exec_multi(p.ptr, ins, outs, batch, 1) == 0
+    assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), oracle_rows(x, 1))
