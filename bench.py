@@ -219,6 +219,10 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config),
                            "kernel": "whole step (event timed)"}
+    # practical HBM ceiling on this device: a 16-B-per-lane stream copy of the same buffers
+    nbytes = min(din.nbytes, dout.nbytes) // 16 * 16
+    cms = hsfft.bench_copy(din, dout, nbytes, 5)
+    out["stream_copy_gbs"] = round(2 * nbytes * 5 / (cms / 1e3) / 1e9, 1)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:

@@ -81,6 +81,10 @@ int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
 int hsfft_time_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out,
                            int batch, int iters, float *ms);
 
+/* Stream-copy reference: `iters` device copies of `bytes` (multiple of 16) from d_src to
+ * d_dst, event-timed; the practical HBM ceiling reported next to the FFT numbers. */
+int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms);
+
 /* --- multi-device (single process; one host thread per device, no collective) --------- */
 /* Shards the batch contiguously over devices 0..ndev-1: h-side arrays of per-device
  * pointers d_in[g], d_out[g] each hold rows [g*batch/ndev, (g+1)*batch/ndev). */

@@ -305,6 +305,13 @@ __global__ void k_copy_rows(const double *src, long long sdist, long long soff, 
         dst[b * ddist + i] = i < ncopy ? src[b * sdist + soff + i] : 0.0;
 }
 
+/* stream copy (practical HBM ceiling for the bench report) */
+__global__ void k_copy16(const double2 *__restrict__ a, double2 *__restrict__ b, long long n)
+{
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
 hipEvent_t g_t0, g_t1;
 bool g_timer_init = false;
 hipEvent_t g_pev[2 * HS_MAX_PASSES];
@@ -461,6 +468,8 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     return 0;
 }
 
+int r8_has_variant(int r0, int n8, int G, int Wq, int first) { return r8::find(r0, n8, G, Wq, first != 0) != nullptr; }
+
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset)
 {
     hipLaunchKernelGGL(k_fill_complex, dim3(4096), dim3(256), 0, stream(), (double2 *)d, (long long)count,
@@ -519,6 +528,23 @@ int hsd_copy_rows(const void *src, long long sdist, long long soff, long long nc
     hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(dlen, 256), batch), dim3(256), 0, stream(), (const double *)src,
                        sdist, soff, ncopy, (double *)dst, ddist, dlen);
     HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *ms)
+{
+    hipEvent_t e0, e1;
+    HCHK(hipEventCreate(&e0));
+    HCHK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_copy16, dim3(256 * 16), dim3(256), 0, stream(), (const double2 *)src, (double2 *)dst, n16);
+    HCHK(hipEventRecord(e0, stream()));
+    for (int i = 0; i < iters; i++)
+        hipLaunchKernelGGL(k_copy16, dim3(256 * 16), dim3(256), 0, stream(), (const double2 *)src, (double2 *)dst, n16);
+    HCHK(hipEventRecord(e1, stream()));
+    HCHK(hipEventSynchronize(e1));
+    HCHK(hipEventElapsedTime(ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
     return 0;
 }
 

@@ -84,10 +84,102 @@ static int pass_pmax(void)
     return v;
 }
 
+static int env_int(const char *name, int dflt)
+{
+    const char *s = getenv(name);
+    return s ? atoi(s) : dflt;
+}
+
+/* Register-kernel schedule for radix lists [r0, 8, 8, ...] (r0 in {2,4,8}; hsfft_pass_r8.h):
+ * first pass [r0, 8^k1] with P <= 2048, then passes of 8^k (k <= 3), as few passes as
+ * possible and as even as possible.  Tiles come from the variant table of the kernel. */
+static int build_passes_pow2(hs_entry *e)
+{
+    const int r0 = e->stage_r[0];
+    if (!e->first_leaf || !(r0 == 2 || r0 == 4 || r0 == 8)) return -1;
+    for (int s = 1; s < e->nst; s++)
+        if (e->stage_r[s] != 8) return -1;
+    if (env_int("HSFFT_GENERIC", 0)) return -1;
+    int n8 = e->nst - 1;            /* radix-8 stages after stage 0 */
+    const int k1max = r0 == 8 ? 2 : 3; /* P <= 2048 and at most 4 stages per pass */
+    /* number of later passes needed if the first takes k1 eights: ceil((n8-k1)/3) */
+    int best_k1 = -1, best_np = 1 << 30, best_bal = 1 << 30;
+    for (int k1 = r0 == 8 ? 0 : 1; k1 <= k1max && k1 <= n8; k1++) { /* every pass needs P >= 8 */
+        const int rest = n8 - k1, np = 1 + (rest + 2) / 3;
+        int bal = 0;
+        if (rest) {
+            const int per = (rest + (np - 1) - 1) / (np - 1);
+            bal = per > k1 + 1 ? per - k1 - 1 : k1 + 1 - per;
+        }
+        const int forced = env_int("HSFFT_K1", -1);
+        if (forced >= 0 && k1 != forced) continue;
+        if (np < best_np || (np == best_np && bal < best_bal)) {
+            best_np = np;
+            best_bal = bal;
+            best_k1 = k1;
+        }
+    }
+    if (best_k1 < 0 || best_np > HS_MAX_PASSES) return -1;
+    long long B = 1;
+    int np = 0, s = 0;
+    const int later = best_np - 1;
+    int remaining = n8 - best_k1;
+    for (int ip = 0; ip < best_np; ip++) {
+        hsd_pass *p = &e->pass[np++];
+        memset(p, 0, sizeof *p);
+        int k = ip == 0 ? best_k1 : (remaining + (later - (ip - 1)) - 1) / (later - (ip - 1));
+        if (ip > 0) remaining -= k;
+        p->nst = ip == 0 ? 1 + k : k;
+        p->P = 1;
+        for (int i = 0; i < p->nst; i++) {
+            p->radix[i] = e->stage_r[s++];
+            p->gcs_off[i] = -1;
+            p->P *= p->radix[i];
+        }
+        p->leaf = ip == 0;
+        p->B = B;
+        p->A = e->M / (B * p->P);
+        p->variant = HS_KV_R8X3;
+        if (ip == 0) {
+            /* WM columns per workgroup: as many as the LDS (<=128 KiB) and the variant table allow */
+            static const int gopts[] = {32, 16, 8, 4, 2, 1};
+            int gmax = env_int("HSFFT_G1", 0);
+            if (gmax <= 0) gmax = p->P >= 2048 ? 4 : p->P >= 1024 ? 4 : p->P >= 512 ? 8 : p->P >= 64 ? 16 : 32;
+            int G = 1;
+            for (unsigned i = 0; i < sizeof gopts / sizeof gopts[0]; i++)
+                if (gopts[i] <= gmax && gopts[i] <= p->A && r8_has_variant(p->radix[0], p->nst - 1, gopts[i], 1, 1)) {
+                    G = gopts[i];
+                    break;
+                }
+            p->Wm = G;
+            p->Wq = 1;
+            p->G = G;
+        } else {
+            static const int gopts[] = {32, 16, 8, 4};
+            int gmax = env_int("HSFFT_G2", 0);
+            if (gmax <= 0) gmax = p->P >= 512 ? 8 : 32;
+            int G = 0;
+            for (unsigned i = 0; i < sizeof gopts / sizeof gopts[0]; i++)
+                if (gopts[i] <= gmax && gopts[i] <= B && r8_has_variant(8, p->nst - 1, gopts[i], gopts[i], 0)) {
+                    G = gopts[i];
+                    break;
+                }
+            if (!G) return -1;
+            p->Wm = 1;
+            p->Wq = G;
+            p->G = G;
+        }
+        B *= p->P;
+    }
+    e->npass = np;
+    return 0;
+}
+
 /* Groups stages into passes of at most Pmax points and chooses the tile so that global
  * loads/stores move >= 128 contiguous bytes (8 complex) per row where the shape allows. */
 static int build_passes(hs_entry *e)
 {
+    if (build_passes_pow2(e) == 0) return 0;
     const int pmax = pass_pmax();
     int s = 0, np = 0;
     long long B = 1;
@@ -226,7 +318,7 @@ static hs_entry *entry_build(const struct fft_set *o)
             e->tw_from_struct = 0;
             e->rlf = factors(e->M, e->rfac);
             e->tw_private = calloc((size_t)e->M, sizeof(fft_data));
-            hs_longvector(e->tw_private, e->M, e->factors, e->lf, hs_twiddle_mode() == 1);
+            hs_longvector(e->tw_private, e->M, e->rfac, e->rlf, hs_twiddle_mode() == 1);
             if (o->sgn == -1)
                 for (int i = 0; i < e->M; i++) e->tw_private[i].im = -e->tw_private[i].im;
         }
@@ -451,6 +543,11 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
         long long per = (long long)(chunk_bytes() / (sizeof(fft_data) * (size_t)M));
         if (per < 1) per = 1;
         if (chunk > per) chunk = per;
+    } else {
+        /* optional: run all passes over a few rows at a time so the intermediate stays in
+         * the 256 MiB Infinity Cache between passes (HSFFT_MALL_ROWS) */
+        const int rows = env_int("HSFFT_MALL_ROWS", 0);
+        if (rows > 0 && chunk > rows) chunk = rows;
     }
     void *S[2] = {NULL, NULL};
     for (int k = 0; k < need; k++) {
@@ -660,6 +757,14 @@ int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
         }
     }
     return 0;
+}
+
+int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms)
+{
+    if (!d_src || !d_dst || !ms || iters < 1 || bytes % 16) return HSFFT_ERR_ARG;
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    return hsd_copy_bench(d_src, d_dst, (long long)(bytes / 16), iters, ms) ? HSFFT_ERR_DEVICE : 0;
 }
 
 int hsfft_exec_multi(fft_object obj, const fft_data *const *d_in, fft_data *const *d_out, int batch, int ndev)

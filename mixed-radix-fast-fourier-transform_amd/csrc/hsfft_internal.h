@@ -79,6 +79,8 @@ int hsd_is_device_ptr(const void *p);
 const char *hsd_errstr(void);
 
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l);
+/* 1 if the register kernel has an instantiation for [r0, 8^n8] with this tile */
+int r8_has_variant(int r0, int n8, int G, int Wq, int first);
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset);
 int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset);
 /* r2c split (real.c:108-132): Z rows of h complex -> X rows of 2h complex */
@@ -93,6 +95,7 @@ int hsd_copy_rows(const void *src, long long sdist, long long soff, long long nc
 
 /* timing on the library stream */
 int hsd_timer_start(void);
+int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *ms);
 int hsd_timer_stop(float *ms);
 int hsd_pass_timer_begin(int i);
 int hsd_pass_timer_end(int i);

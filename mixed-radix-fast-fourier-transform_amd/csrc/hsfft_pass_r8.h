@@ -1,10 +1,327 @@
-/* hsfft_pass_r8.h -- specialised register-resident passes (filled in by the next milestone). */
+/*
+ * hsfft_pass_r8.h -- register-resident Stockham passes for power-of-two radix lists
+ * (radix 2/4 first, then radix 8): the hot path of BASELINE configs 2 (2^20 = [4,8^6]),
+ * 4 (Bluestein M = 2^18 = [8^6]) and 5 (r2c inner 2^21 = [8^7]).
+ *
+ * One workgroup transforms G groups (G = WM x WQ tile of (m, q) pairs, hsfft_internal.h) of
+ * P = R0 * 8^N8 points.  Every thread owns 8 points of one group in registers for every
+ * stage (8/R butterflies of radix R); stages hand data over through one LDS image
+ * (index p*G + g), so the only global traffic is the pass's input read and output write
+ * plus the plan's twiddles.  Index arithmetic is compile-time (shifts / masks).
+ *
+ * Arithmetic is the reference's (butterflies in hsfft_butterfly.h, twiddles from the plan's
+ * own table, -ffp-contract=off), so the results are bit-identical to the generic kernel.
+ */
 #pragma once
 
 namespace r8 {
-inline int launch(const hsd_pass *, const hsd_launch *, hipStream_t)
+
+struct Args {
+    const double2 *in;
+    double2 *out;
+    const double2 *tw;
+    const double2 *laux, *saux;
+    long long idist, odist, A, B, nsig, tiles_q, tiles;
+    int sgn, dir, conj, load_op, store_op;
+    int xcd_groups;   /* >0: remap block ids so that consecutive tiles share an XCD */
+    int tile_major;   /* 1: block order tile-major (all rows of a tile adjacent) */
+    long long batch;
+};
+
+template <int N>
+struct ilog2 {
+    static constexpr int v = 1 + ilog2<N / 2>::v;
+};
+template <>
+struct ilog2<1> {
+    static constexpr int v = 0;
+};
+
+template <int R0, int N8>
+struct Shape {
+    static constexpr int NST = 1 + N8;
+    static constexpr int P = R0 * (N8 >= 1 ? 8 : 1) * (N8 >= 2 ? 8 : 1) * (N8 >= 3 ? 8 : 1) * (N8 >= 4 ? 8 : 1);
+    static constexpr int TPG = P / 8;
+    /* radix and local L of stage s */
+    static constexpr int R(int s) { return s == 0 ? R0 : 8; }
+    static constexpr int Lloc(int s) { return s == 0 ? 1 : R0 * (s >= 2 ? 8 : 1) * (s >= 3 ? 8 : 1) * (s >= 4 ? 8 : 1); }
+};
+
+/* apply the stage's twiddles and butterflies to the 8 registers (8/R butterflies) */
+template <int R, int LLOC, int TPG>
+__device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const Args &a, int jt, long long q,
+                                         bool first_pass, bool valid)
 {
-    snprintf(g_err, sizeof g_err, "specialised pass variant not built");
-    return -4;
+    constexpr int NB = 8 / R;
+    const long long L = a.B * LLOC;
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        const int b = c * TPG + jt;
+        const int kloc = b & (LLOC - 1);
+        if (!first_pass) {
+            const long long k = q + a.B * kloc;
+            /* radix-4 combine skips the k == 0 column (ref :826-855); 2 and 8 never skip */
+            if (valid && !(R == 4 && k == 0)) {
+                const double2 *w = a.tw + (L - 1 + (long long)(R - 1) * k);
+#pragma unroll
+                for (int i = 1; i < R; i++) {
+                    const double2 t = w[i - 1];
+                    hsb::twmul(xr[c * R + i], xi[c * R + i], t.x, a.conj ? -t.y : t.y);
+                }
+            }
+        }
+        hsb::bfly<R>(&xr[c * R], &xi[c * R], a.sgn, first_pass);
+    }
 }
+
+/* stage s outputs -> LDS -> stage s+1 inputs.  SPLIT exchanges the real parts, then the
+ * imaginary parts, through a P*G-double image (half the LDS, so twice the workgroups per CU). */
+template <int R, int LLOC, int R2, int TPG, int P, int G, bool SPLIT>
+__device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], double2 *lds, int jt, int g)
+{
+    constexpr int NB = 8 / R, NB2 = 8 / R2, L2 = LLOC * R, S2 = P / (L2 * R2);
+    if constexpr (!SPLIT) {
+#pragma unroll
+        for (int c = 0; c < NB; c++) {
+            const int b = c * TPG + jt;
+            const int kloc = b & (LLOC - 1), ml = b / LLOC;
+#pragma unroll
+            for (int jj = 0; jj < R; jj++) {
+                const int p = ml * LLOC * R + kloc + jj * LLOC;
+                lds[p * G + g] = make_double2(xr[c * R + jj], xi[c * R + jj]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < NB2; c++) {
+            const int b = c * TPG + jt;
+            const int kloc = b & (L2 - 1), ml = b / L2;
+#pragma unroll
+            for (int i = 0; i < R2; i++) {
+                const int p = (ml + i * S2) * L2 + kloc;
+                const double2 v = lds[p * G + g];
+                xr[c * R2 + i] = v.x;
+                xi[c * R2 + i] = v.y;
+            }
+        }
+        __syncthreads();
+    } else {
+        double *ld = reinterpret_cast<double *>(lds);
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            double(&x)[8] = part ? xi : xr;
+#pragma unroll
+            for (int c = 0; c < NB; c++) {
+                const int b = c * TPG + jt;
+                const int kloc = b & (LLOC - 1), ml = b / LLOC;
+#pragma unroll
+                for (int jj = 0; jj < R; jj++) ld[(ml * LLOC * R + kloc + jj * LLOC) * G + g] = x[c * R + jj];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < NB2; c++) {
+                const int b = c * TPG + jt;
+                const int kloc = b & (L2 - 1), ml = b / L2;
+#pragma unroll
+                for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[((ml + i * S2) * L2 + kloc) * G + g];
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ double2 load_hook(const Args &a, const double2 *in, long long n)
+{
+    if (a.load_op == HS_LOAD_CHIRP) {
+        if (n >= a.nsig) return make_double2(0.0, 0.0);
+        const double2 x = in[n], h = a.laux[n];
+        if (a.dir == 1) return make_double2(x.x * h.x + x.y * h.y, -x.x * h.y + x.y * h.x);
+        return make_double2(x.x * h.x - x.y * h.y, x.x * h.y + x.y * h.x);
+    }
+    return in[n];
+}
+
+__device__ __forceinline__ void store_hook(const Args &a, double2 *out, long long n, double yr, double yi)
+{
+    if (a.store_op == HS_STORE_PLAIN) {
+        out[n] = make_double2(yr, yi);
+    } else if (a.store_op == HS_STORE_SPEC) {
+        const double2 k = a.saux[n];
+        if (a.dir == 1) out[n] = make_double2(yr * k.x - yi * k.y, yr * k.y + yi * k.x);
+        else out[n] = make_double2(yr * k.x + yi * k.y, -yr * k.y + yi * k.x);
+    } else if (n < a.nsig) {
+        const double2 h = a.saux[n];
+        if (a.dir == 1) out[n] = make_double2(yr * h.x + yi * h.y, -yr * h.y + yi * h.x);
+        else out[n] = make_double2(yr * h.x - yi * h.y, yr * h.y + yi * h.x);
+    }
+}
+
+template <int R0, int N8, int G, int WQ, bool FIRST, bool SPLIT>
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
+{
+    using S = Shape<R0, N8>;
+    constexpr int P = S::P, TPG = S::TPG, WM = G / WQ;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+
+    long long blk = blockIdx.x;
+    if (a.xcd_groups > 0) { /* bijective XCD remap (cdna_hip_programming.md §5 'XCD swizzle') */
+        const long long nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blk % 8;
+        blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blk / 8;
+    }
+    const long long b = a.tile_major ? blk % a.batch : blk / a.tiles;
+    const long long tile = a.tile_major ? blk / a.batch : blk % a.tiles;
+    const int tid = threadIdx.x, g = tid % G, jt = tid / G;
+    const long long m = (tile / a.tiles_q) * WM + g / WQ;
+    const long long q = FIRST ? 0 : (tile % a.tiles_q) * WQ + g % WQ;
+    const bool valid = m < a.A && q < a.B;
+    const double2 *in = a.in + b * a.idist;
+    double2 *out = a.out + b * a.odist;
+
+    double xr[8], xi[8];
+    { /* stage-0 inputs straight from global memory: t = c*TPG + jt + i*(P/R0) */
+        constexpr int R = R0, NB = 8 / R0, S0 = P / R0;
+#pragma unroll
+        for (int c = 0; c < NB; c++)
+#pragma unroll
+            for (int i = 0; i < R; i++) {
+                const long long t = c * TPG + jt + i * S0;
+                double2 v = make_double2(0.0, 0.0);
+                if (valid) v = load_hook(a, in, (t * a.A + m) * a.B + q);
+                xr[c * R + i] = v.x;
+                xi[c * R + i] = v.y;
+            }
+    }
+
+    do_stage<R0, 1, TPG>(xr, xi, a, jt, q, FIRST, valid);
+    if constexpr (N8 >= 1) {
+        exchange<R0, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+        do_stage<8, S::Lloc(1), TPG>(xr, xi, a, jt, q, false, valid);
+    }
+    if constexpr (N8 >= 2) {
+        exchange<8, S::Lloc(1), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+        do_stage<8, S::Lloc(2), TPG>(xr, xi, a, jt, q, false, valid);
+    }
+    if constexpr (N8 >= 3) {
+        exchange<8, S::Lloc(2), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+        do_stage<8, S::Lloc(3), TPG>(xr, xi, a, jt, q, false, valid);
+    }
+
+    /* last stage: ml == 0, output u = kloc + jj*LL, written to [m][u][q] */
+    constexpr int RL = S::R(S::NST - 1), LL = S::Lloc(S::NST - 1), NBL = 8 / RL;
+    if (!valid) return;
+#pragma unroll
+    for (int c = 0; c < NBL; c++) {
+        const int kloc = c * TPG + jt;
+#pragma unroll
+        for (int jj = 0; jj < RL; jj++) {
+            const long long u = kloc + jj * LL;
+            store_hook(a, out, (m * P + u) * a.B + q, xr[c * RL + jj], xi[c * RL + jj]);
+        }
+    }
+}
+
+typedef void (*kfn)(Args);
+
+struct Variant {
+    int r0, n8, G, WQ;
+    bool first, split;
+    kfn fn;
+};
+
+#define R8V(r0, n8, g, wq, f) {r0, n8, g, wq, f, false, k_pass<r0, n8, g, wq, f, false>}, \
+                              {r0, n8, g, wq, f, true, k_pass<r0, n8, g, wq, f, true>}
+static const Variant k_variants[] = {
+    /* first passes (B == 1): WQ = 1, G = WM */
+    R8V(4, 3, 1, 1, true), R8V(4, 3, 2, 1, true), R8V(4, 3, 4, 1, true),
+    R8V(2, 3, 1, 1, true), R8V(2, 3, 2, 1, true), R8V(2, 3, 4, 1, true),
+    R8V(8, 2, 1, 1, true), R8V(8, 2, 2, 1, true), R8V(8, 2, 4, 1, true), R8V(8, 2, 8, 1, true),
+    R8V(4, 2, 1, 1, true), R8V(4, 2, 4, 1, true), R8V(4, 2, 8, 1, true),
+    R8V(2, 2, 1, 1, true), R8V(2, 2, 4, 1, true), R8V(2, 2, 8, 1, true),
+    R8V(8, 1, 1, 1, true), R8V(8, 1, 8, 1, true), R8V(8, 1, 16, 1, true),
+    R8V(4, 1, 1, 1, true), R8V(4, 1, 16, 1, true), R8V(4, 1, 32, 1, true),
+    R8V(2, 1, 1, 1, true), R8V(2, 1, 16, 1, true),
+    R8V(8, 0, 1, 1, true), R8V(8, 0, 16, 1, true),
+    /* later passes: radix-8 only, WQ = G (tiles along q) */
+    R8V(8, 2, 8, 8, false), R8V(8, 2, 4, 4, false), R8V(8, 2, 16, 16, false),
+    R8V(8, 1, 8, 8, false), R8V(8, 1, 16, 16, false), R8V(8, 1, 32, 32, false),
+    R8V(8, 0, 8, 8, false), R8V(8, 0, 32, 32, false),
+};
+#undef R8V
+
+inline const Variant *find(int r0, int n8, int G, int WQ, bool first, bool split = false)
+{
+    for (const Variant &v : k_variants)
+        if (v.r0 == r0 && v.n8 == n8 && v.G == G && v.WQ == WQ && v.first == first && v.split == split) return &v;
+    return nullptr;
+}
+
+inline int split_mode(bool first)
+{
+    static int m = -1;
+    if (m < 0) {
+        const char *e = getenv("HSFFT_SPLIT");
+        m = e ? atoi(e) : 0;
+    }
+    return first ? (m & 1) : ((m >> 1) & 1);
+}
+
+inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
+{
+    /* the pass's radices must be [r0, 8, 8, ...] with r0 in {2,4,8} */
+    int n8 = p->nst - 1;
+    const bool first = p->B == 1;
+    const bool split = split_mode(first) && p->nst > 1;
+    const Variant *v = find(p->radix[0], n8, p->G, p->Wq, first, split);
+    for (int s = 1; s < p->nst; s++)
+        if (p->radix[s] != 8) v = nullptr;
+    if (!v || (first && !p->leaf) || p->Wm * p->Wq != p->G) {
+        snprintf(g_err, sizeof g_err, "r8: no kernel variant for this pass (P=%d G=%d Wq=%d)", p->P, p->G, p->Wq);
+        return -4;
+    }
+    Args a;
+    a.in = (const double2 *)l->in;
+    a.out = (double2 *)l->out;
+    a.tw = (const double2 *)l->tw;
+    a.laux = (const double2 *)l->load_aux;
+    a.saux = (const double2 *)l->store_aux;
+    a.idist = l->idist;
+    a.odist = l->odist;
+    a.A = p->A;
+    a.B = p->B;
+    a.nsig = l->nsig;
+    a.sgn = l->sgn;
+    a.dir = l->dir;
+    a.conj = l->conj;
+    a.load_op = l->load_op;
+    a.store_op = l->store_op;
+    /* measured on MI355X (profiles/): the XCD remap keeps neighbouring tiles of one row on
+     * one L2; HSFFT_ORDER bit0/bit1 make the first / later passes tile-major */
+    static int xcd = -1, order = -1;
+    if (xcd < 0) {
+        const char *e1 = getenv("HSFFT_XCD"), *e2 = getenv("HSFFT_ORDER");
+        xcd = e1 ? atoi(e1) : 1;
+        order = e2 ? atoi(e2) : 0;
+    }
+    a.xcd_groups = xcd;
+    a.tile_major = first ? (order & 1) : ((order >> 1) & 1);
+    a.batch = l->batch;
+    const long long tm = (p->A + p->Wm - 1) / p->Wm, tq = (p->B + p->Wq - 1) / p->Wq;
+    a.tiles_q = tq;
+    a.tiles = tm * tq;
+    const long long grid = a.tiles * l->batch;
+    const int threads = (p->P / 8) * p->G;
+    const size_t lds = (size_t)p->P * p->G * (split ? sizeof(double) : sizeof(double2));
+    if (grid <= 0 || grid > 0x7fffffffLL || threads > 1024 || lds > 160 * 1024) {
+        snprintf(g_err, sizeof g_err, "r8: bad geometry grid=%lld threads=%d lds=%zu", grid, threads, lds);
+        return -1;
+    }
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void *)v->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return set_err(e, "hipFuncSetAttribute");
+    }
+    hipLaunchKernelGGL(v->fn, dim3((unsigned)grid), dim3(threads), lds, st, a);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
 }  // namespace r8

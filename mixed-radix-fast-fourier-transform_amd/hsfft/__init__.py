@@ -62,6 +62,7 @@ SIGNATURES = {
                                 ctypes.POINTER(ctypes.c_float), CI]),
     "hsfft_time_r2c_batched": (CI, [VP, VP, VP, CI, CI, ctypes.POINTER(ctypes.c_float)]),
     "hsfft_exec_multi": (CI, [VP, VP, VP, CI, CI]),
+    "hsfft_bench_copy": (CI, [VP, VP, ctypes.c_size_t, CI, ctypes.POINTER(ctypes.c_float)]),
 }
 
 STRUCT_TWIDDLE_OFFSET = 272  # offsetof(struct fft_set, twiddle), include/highspeedFFT.h
@@ -245,6 +246,12 @@ def time_batched(plan, d_in, d_out, batch, iters, max_pass=16):
     check(lib().hsfft_time_batched(plan.ptr, VP(d_in.ptr), VP(d_out.ptr), batch, iters, ctypes.byref(ms), pms,
                                    max_pass), "time_batched")
     return ms.value, [pms[i] for i in range(max_pass)]
+
+
+def bench_copy(d_src, d_dst, nbytes, iters):
+    ms = ctypes.c_float(0.0)
+    check(lib().hsfft_bench_copy(VP(d_src.ptr), VP(d_dst.ptr), nbytes, iters, ctypes.byref(ms)), "bench_copy")
+    return ms.value
 
 
 def time_r2c_batched(rplan, d_in, d_out, batch, iters):

@@ -245,7 +245,8 @@ def test_divergences_d3_d5_d6():
             y = hsfft.Plan(n, sgn).exec(x)
             assert T.bits_equal(y, oracle_rows(x, sgn)), (n, sgn)
             X = np.fft.fft(x) if sgn == 1 else np.fft.ifft(x) * n
-            assert np.abs(y - X).max() <= 1e-12 * max(1.0, np.abs(X).max()), n
+            # 1025 = 5^2*41 is mixed radix with the reference's 11-digit radix-5 constants
+            assert np.abs(y - X).max() <= 1e-10 * max(1.0, np.abs(X).max()), n
 
 
 def test_generic_odd_radices():
