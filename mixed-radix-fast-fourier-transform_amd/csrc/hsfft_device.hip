@@ -39,7 +39,11 @@ int set_err(hipError_t e, const char *what)
         if (e_ != hipSuccess) return set_err(e_, #call);                \
     } while (0)
 
-hipStream_t stream()
+hipStream_t g_stream2[HS_MAX_DEV];
+bool g_stream2_init[HS_MAX_DEV];
+thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline stream */
+
+hipStream_t primary()
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) dev = 0;
@@ -49,6 +53,24 @@ hipStream_t stream()
     }
     return g_stream[dev];
 }
+
+/* the stream kernels are launched on: the library stream, or (inside a pipelined chain)
+ * the second stream that runs pass B of chunk c while pass A of chunk c+1 runs */
+hipStream_t stream()
+{
+    if (t_sidx == 0) return primary();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) dev = 0;
+    if (!g_stream2_init[dev]) {
+        if (hipStreamCreateWithFlags(&g_stream2[dev], hipStreamNonBlocking) != hipSuccess) g_stream2[dev] = 0;
+        g_stream2_init[dev] = true;
+    }
+    return g_stream2[dev];
+}
+
+#define HS_NEV 64
+hipEvent_t g_ev[HS_MAX_DEV][HS_NEV];
+bool g_ev_init[HS_MAX_DEV];
 
 /* ------------------------------------------------------------------ generic pass kernel */
 struct KArgs {
@@ -312,6 +334,30 @@ __global__ void k_copy16(const double2 *__restrict__ a, double2 *__restrict__ b,
         b[i] = a[i];
 }
 
+/* copy variants for the HBM access-pattern study (tools/membench.py) */
+typedef double v2d __attribute__((ext_vector_type(2)));
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_copyU(const v2d *__restrict__ a, v2d *__restrict__ b, long long n)
+{
+    const long long stride = (long long)gridDim.x * blockDim.x * U;
+    for (long long base = blockIdx.x * (long long)blockDim.x * U + threadIdx.x; base < n; base += stride) {
+        v2d v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long long i = base + (long long)u * blockDim.x;
+            if (i < n) v[u] = NT ? __builtin_nontemporal_load(&a[i]) : a[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long long i = base + (long long)u * blockDim.x;
+            if (i < n) {
+                if (NT) __builtin_nontemporal_store(v[u], &b[i]);
+                else b[i] = v[u];
+            }
+        }
+    }
+}
+
 hipEvent_t g_t0, g_t1;
 bool g_timer_init = false;
 hipEvent_t g_pev[2 * HS_MAX_PASSES];
@@ -397,11 +443,39 @@ int hsd_memset_async(void *d, int v, size_t bytes)
 
 int hsd_sync(void)
 {
-    HCHK(hipStreamSynchronize(stream()));
+    HCHK(hipStreamSynchronize(primary()));
     return 0;
 }
 
-void *hsd_stream(void) { return (void *)stream(); }
+int hsd_select_stream(int idx)
+{
+    t_sidx = idx ? 1 : 0;
+    return 0;
+}
+
+/* event ring for cross-stream ordering: record slot i on the current stream / make the
+ * current stream wait for slot i's most recent record */
+int hsd_event_record(int i)
+{
+    int dev = hsd_get_device();
+    if (dev < 0 || dev >= HS_MAX_DEV) return -1;
+    if (!g_ev_init[dev]) {
+        for (int k = 0; k < HS_NEV; k++) HCHK(hipEventCreateWithFlags(&g_ev[dev][k], hipEventDisableTiming));
+        g_ev_init[dev] = true;
+    }
+    HCHK(hipEventRecord(g_ev[dev][i % HS_NEV], stream()));
+    return 0;
+}
+
+int hsd_event_wait(int i)
+{
+    int dev = hsd_get_device();
+    if (dev < 0 || dev >= HS_MAX_DEV || !g_ev_init[dev]) return -1;
+    HCHK(hipStreamWaitEvent(stream(), g_ev[dev][i % HS_NEV], 0));
+    return 0;
+}
+
+void *hsd_stream(void) { return (void *)primary(); }
 
 int hsd_is_device_ptr(const void *p)
 {
@@ -543,8 +617,29 @@ int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *
     HCHK(hipEventRecord(e1, stream()));
     HCHK(hipEventSynchronize(e1));
     HCHK(hipEventElapsedTime(ms, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+extern "C" int hsd_copy_bench_v(const void *src, void *dst, long long n16, int iters, int variant, int grid, float *ms)
+{
+    typedef void (*cfn)(const v2d *, v2d *, long long);
+    static const cfn fns[] = {k_copyU<1, false>, k_copyU<4, false>, k_copyU<8, false>,
+                              k_copyU<1, true>, k_copyU<4, true>, k_copyU<8, true>};
+    if (variant < 0 || variant >= 6) return -1;
+    hipEvent_t e0, e1;
+    HCHK(hipEventCreate(&e0));
+    HCHK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(fns[variant], dim3(grid), dim3(256), 0, stream(), (const v2d *)src, (v2d *)dst, n16);
+    HCHK(hipEventRecord(e0, stream()));
+    for (int i = 0; i < iters; i++)
+        hipLaunchKernelGGL(fns[variant], dim3(grid), dim3(256), 0, stream(), (const v2d *)src, (v2d *)dst, n16);
+    HCHK(hipEventRecord(e1, stream()));
+    HCHK(hipEventSynchronize(e1));
+    HCHK(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return 0;
 }
 

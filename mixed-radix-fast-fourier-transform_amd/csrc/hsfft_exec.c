@@ -511,8 +511,48 @@ static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long
     l.store_op = store_op;
     l.store_aux = saux;
     l.nsig = nsig;
+    /* HSFFT_NT bit0/1: first pass nt load/store, bit2/3: last pass nt load/store */
+    const int nt = env_int("HSFFT_NT", 0);
+    if (i == 0) {
+        l.nt_load = nt & 1;
+        l.nt_store = (nt >> 1) & 1;
+    }
+    if (i == e->npass - 1) {
+        l.nt_load |= (nt >> 2) & 1;
+        l.nt_store |= (nt >> 3) & 1;
+    }
+    if (env_int("HSFFT_DEV_ALIAS", 0)) l.idist = l.odist = 0; /* dev probe: MALL-resident timing only */
     int rc = hsd_run_pass(&e->pass[i], &l);
     if (rc) hs_seterr("pass %d: %s", i, hsd_errstr());
+    return rc;
+}
+
+/* Two-pass chain over the batch in chunks of `chunk` rows, software-pipelined over two
+ * streams: pass A of chunk k+1 (library stream) overlaps pass B of chunk k (second stream),
+ * ordered by events; at most `lag` chunks run ahead so the in-flight intermediates stay in
+ * the 256 MiB Infinity Cache.  The library stream waits for the last pass B at the end. */
+static int run_pipelined(hs_entry *e, hs_devstate *ds, const void *I, long long idist, void *O, long long odist,
+                         int batch, int chunk, int sgn, int conj, int dir, int load_op, const void *laux,
+                         int store_op, const void *saux, long long nsig)
+{
+    const int lag = env_int("HSFFT_PIPE_LAG", 2);
+    int rc = 0, k = 0;
+    for (long long c0 = 0; c0 < batch && !rc; c0 += chunk, k++) {
+        const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
+        fft_data *W = (fft_data *)O + c0 * odist;
+        hsd_select_stream(0);
+        if (k >= lag) rc = hsd_event_wait(2 * (k - lag) + 1); /* pass B of chunk k-lag done */
+        if (!rc) rc = launch_pass(e, ds, 0, (const fft_data *)I + c0 * idist, idist, W, odist, cb, sgn, conj, dir,
+                                  load_op, laux, HS_STORE_PLAIN, NULL, nsig);
+        if (!rc) rc = hsd_event_record(2 * k);
+        hsd_select_stream(1);
+        if (!rc) rc = hsd_event_wait(2 * k);
+        if (!rc) rc = launch_pass(e, ds, 1, W, odist, W, odist, cb, sgn, conj, dir, HS_LOAD_PLAIN, NULL, store_op,
+                                  saux, nsig);
+        if (!rc) rc = hsd_event_record(2 * k + 1);
+    }
+    hsd_select_stream(0);
+    if (!rc && k > 0) rc = hsd_event_wait(2 * (k - 1) + 1);
     return rc;
 }
 
@@ -557,6 +597,9 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
             return HSFFT_ERR_NOMEM;
         }
     }
+    if (!need && n == 2 && chunk < batch && env_int("HSFFT_PIPE", 0))
+        return run_pipelined(e, ds, I, idist, O, odist, batch, (int)chunk, sgn, conj, dir, load_op, laux, store_op,
+                             saux, nsig);
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         const void *R = (const fft_data *)I + c0 * idist;

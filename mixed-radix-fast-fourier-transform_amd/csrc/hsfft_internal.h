@@ -61,6 +61,7 @@ typedef struct {
     int load_op, store_op;
     const void *load_aux, *store_aux;
     long long nsig;
+    int nt_load, nt_store;          /* non-temporal input / output (register kernels) */
 } hsd_launch;
 
 /* device layer (hsfft_device.hip) */
@@ -74,6 +75,9 @@ int hsd_d2h(void *h, const void *d, size_t bytes);
 int hsd_d2d_async(void *d, const void *s, size_t bytes);
 int hsd_memset_async(void *d, int v, size_t bytes);
 int hsd_sync(void);
+int hsd_select_stream(int idx);   /* 0 library stream, 1 pipeline stream (this thread) */
+int hsd_event_record(int i);      /* event ring (64 slots) on the selected stream */
+int hsd_event_wait(int i);
 void *hsd_stream(void);
 int hsd_is_device_ptr(const void *p);
 const char *hsd_errstr(void);

@@ -26,6 +26,7 @@ struct Args {
     int xcd_groups;   /* >0: remap block ids so that consecutive tiles share an XCD */
     int tile_major;   /* 1: block order tile-major (all rows of a tile adjacent) */
     long long batch;
+    int dev_twq;      /* development probe only: twiddle column = q (wrong results, timing) */
 };
 
 template <int N>
@@ -47,30 +48,47 @@ struct Shape {
     static constexpr int Lloc(int s) { return s == 0 ? 1 : R0 * (s >= 2 ? 8 : 1) * (s >= 3 ? 8 : 1) * (s >= 4 ? 8 : 1); }
 };
 
-/* apply the stage's twiddles and butterflies to the 8 registers (8/R butterflies) */
+/* Twiddles of one stage for this thread's 8/R butterflies: tw[L-1 + (R-1)*k + i-1] with
+ * k = q + B*kloc (ref :731-741 and the per-radix combine loops).  Loaded one stage ahead of
+ * their use so the (L2/Infinity-Cache) latency overlaps the previous stage's work. */
 template <int R, int LLOC, int TPG>
-__device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const Args &a, int jt, long long q,
-                                         bool first_pass, bool valid)
+__device__ __forceinline__ void load_tw(double2 (&w)[7], const Args &a, int jt, long long q, bool valid)
 {
     constexpr int NB = 8 / R;
     const long long L = a.B * LLOC;
 #pragma unroll
     for (int c = 0; c < NB; c++) {
-        const int b = c * TPG + jt;
-        const int kloc = b & (LLOC - 1);
-        if (!first_pass) {
-            const long long k = q + a.B * kloc;
+        const int kloc = (c * TPG + jt) & (LLOC - 1);
+        /* invalid lanes read column 0 (always in range): no branch around the loads, which
+         * would make hipcc wait vmcnt(0) after each one */
+        const long long k = valid ? q + (a.dev_twq ? 0 : a.B * kloc) : 0;
+        const double2 *p = a.tw + (L - 1 + (long long)(R - 1) * k);
+#pragma unroll
+        for (int i = 1; i < R; i++) w[c * (R - 1) + i - 1] = p[i - 1];
+    }
+}
+
+/* apply the stage's twiddles (unless this is the leaf) and the 8/R butterflies */
+template <int R, int LLOC, int TPG>
+__device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const double2 (&w)[7], const Args &a,
+                                         int jt, long long q, bool leaf)
+{
+    constexpr int NB = 8 / R;
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        if (!leaf) {
+            const int kloc = (c * TPG + jt) & (LLOC - 1);
             /* radix-4 combine skips the k == 0 column (ref :826-855); 2 and 8 never skip */
-            if (valid && !(R == 4 && k == 0)) {
-                const double2 *w = a.tw + (L - 1 + (long long)(R - 1) * k);
+            const bool skip = R == 4 && q == 0 && kloc == 0;
+            if (!skip) {
 #pragma unroll
                 for (int i = 1; i < R; i++) {
-                    const double2 t = w[i - 1];
+                    const double2 t = w[c * (R - 1) + i - 1];
                     hsb::twmul(xr[c * R + i], xi[c * R + i], t.x, a.conj ? -t.y : t.y);
                 }
             }
         }
-        hsb::bfly<R>(&xr[c * R], &xi[c * R], a.sgn, first_pass);
+        hsb::bfly<R>(&xr[c * R], &xi[c * R], a.sgn, leaf);
     }
 }
 
@@ -130,15 +148,13 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
     }
 }
 
-__device__ __forceinline__ double2 load_hook(const Args &a, const double2 *in, long long n)
+/* Bluestein hooks (ref :1803-1827, :1838-1855, :1871-1886), applied to values that were
+ * loaded unconditionally (no per-element branch around a load) */
+__device__ __forceinline__ double2 chirp_in(const Args &a, double2 x, double2 h, bool inside)
 {
-    if (a.load_op == HS_LOAD_CHIRP) {
-        if (n >= a.nsig) return make_double2(0.0, 0.0);
-        const double2 x = in[n], h = a.laux[n];
-        if (a.dir == 1) return make_double2(x.x * h.x + x.y * h.y, -x.x * h.y + x.y * h.x);
-        return make_double2(x.x * h.x - x.y * h.y, x.x * h.y + x.y * h.x);
-    }
-    return in[n];
+    if (!inside) return make_double2(0.0, 0.0);
+    if (a.dir == 1) return make_double2(x.x * h.x + x.y * h.y, -x.x * h.y + x.y * h.x);
+    return make_double2(x.x * h.x - x.y * h.y, x.x * h.y + x.y * h.x);
 }
 
 __device__ __forceinline__ void store_hook(const Args &a, double2 *out, long long n, double yr, double yi)
@@ -156,54 +172,68 @@ __device__ __forceinline__ void store_hook(const Args &a, double2 *out, long lon
     }
 }
 
-template <int R0, int N8, int G, int WQ, bool FIRST, bool SPLIT>
+template <int R0, int N8, int G, int WQ, bool FIRST, bool SPLIT, bool HOOK>
 __global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
 {
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG, WM = G / WQ;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
 
-    long long blk = blockIdx.x;
+    /* block -> (row b, tile): 32-bit arithmetic (64-bit division expands to long loops) */
+    unsigned blk = blockIdx.x;
     if (a.xcd_groups > 0) { /* bijective XCD remap (cdna_hip_programming.md §5 'XCD swizzle') */
-        const long long nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blk % 8;
+        const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blk % 8;
         blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blk / 8;
     }
-    const long long b = a.tile_major ? blk % a.batch : blk / a.tiles;
-    const long long tile = a.tile_major ? blk / a.batch : blk % a.tiles;
+    const unsigned tiles = (unsigned)a.tiles, nb = (unsigned)a.batch, tq = (unsigned)a.tiles_q;
+    const unsigned b = a.tile_major ? blk % nb : blk / tiles;
+    const unsigned tile = a.tile_major ? blk / nb : blk % tiles;
     const int tid = threadIdx.x, g = tid % G, jt = tid / G;
-    const long long m = (tile / a.tiles_q) * WM + g / WQ;
-    const long long q = FIRST ? 0 : (tile % a.tiles_q) * WQ + g % WQ;
+    const long long m = (long long)(tile / tq) * WM + g / WQ;
+    const long long q = FIRST ? 0 : (long long)(tile % tq) * WQ + g % WQ;
     const bool valid = m < a.A && q < a.B;
-    const double2 *in = a.in + b * a.idist;
-    double2 *out = a.out + b * a.odist;
+    const double2 *in = a.in + (long long)b * a.idist;
+    double2 *out = a.out + (long long)b * a.odist;
 
     double xr[8], xi[8];
-    { /* stage-0 inputs straight from global memory: t = c*TPG + jt + i*(P/R0) */
+    { /* stage-0 inputs straight from global memory: t = c*TPG + jt + i*(P/R0); all loads are
+       * issued unconditionally (clamped index) so they stay in flight together */
         constexpr int R = R0, NB = 8 / R0, S0 = P / R0;
+        const bool chirp = HOOK && a.load_op == HS_LOAD_CHIRP;
 #pragma unroll
         for (int c = 0; c < NB; c++)
 #pragma unroll
             for (int i = 0; i < R; i++) {
                 const long long t = c * TPG + jt + i * S0;
-                double2 v = make_double2(0.0, 0.0);
-                if (valid) v = load_hook(a, in, (t * a.A + m) * a.B + q);
+                const long long n = valid ? (t * a.A + m) * a.B + q : 0;
+                const bool inside = !chirp || n < a.nsig;
+                const long long nl = inside ? n : 0;
+                double2 v = in[nl];
+                if constexpr (HOOK) {
+                    if (chirp) v = chirp_in(a, v, a.laux[nl], inside);
+                }
                 xr[c * R + i] = v.x;
                 xi[c * R + i] = v.y;
             }
     }
 
-    do_stage<R0, 1, TPG>(xr, xi, a, jt, q, FIRST, valid);
+    double2 wa[7], wb[7];
+    if constexpr (!FIRST) load_tw<R0, 1, TPG>(wa, a, jt, q, valid);
+    if constexpr (N8 >= 1) load_tw<8, S::Lloc(1), TPG>(wb, a, jt, q, valid);
+    do_stage<R0, 1, TPG>(xr, xi, wa, a, jt, q, FIRST);
     if constexpr (N8 >= 1) {
+        if constexpr (N8 >= 2) load_tw<8, S::Lloc(2), TPG>(wa, a, jt, q, valid);
         exchange<R0, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
-        do_stage<8, S::Lloc(1), TPG>(xr, xi, a, jt, q, false, valid);
+        do_stage<8, S::Lloc(1), TPG>(xr, xi, wb, a, jt, q, false);
     }
     if constexpr (N8 >= 2) {
+        if constexpr (N8 >= 3) load_tw<8, S::Lloc(3), TPG>(wb, a, jt, q, valid);
         exchange<8, S::Lloc(1), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
-        do_stage<8, S::Lloc(2), TPG>(xr, xi, a, jt, q, false, valid);
+        do_stage<8, S::Lloc(2), TPG>(xr, xi, wa, a, jt, q, false);
     }
     if constexpr (N8 >= 3) {
         exchange<8, S::Lloc(2), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
-        do_stage<8, S::Lloc(3), TPG>(xr, xi, a, jt, q, false, valid);
+        do_stage<8, S::Lloc(3), TPG>(xr, xi, wb, a, jt, q, false);
     }
 
     /* last stage: ml == 0, output u = kloc + jj*LL, written to [m][u][q] */
@@ -214,8 +244,9 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
         const int kloc = c * TPG + jt;
 #pragma unroll
         for (int jj = 0; jj < RL; jj++) {
-            const long long u = kloc + jj * LL;
-            store_hook(a, out, (m * P + u) * a.B + q, xr[c * RL + jj], xi[c * RL + jj]);
+            const long long n = (m * P + kloc + jj * LL) * a.B + q;
+            if constexpr (HOOK) store_hook(a, out, n, xr[c * RL + jj], xi[c * RL + jj]);
+            else out[n] = make_double2(xr[c * RL + jj], xi[c * RL + jj]);
         }
     }
 }
@@ -224,12 +255,15 @@ typedef void (*kfn)(Args);
 
 struct Variant {
     int r0, n8, G, WQ;
-    bool first, split;
+    bool first, split, hook;
     kfn fn;
 };
 
-#define R8V(r0, n8, g, wq, f) {r0, n8, g, wq, f, false, k_pass<r0, n8, g, wq, f, false>}, \
-                              {r0, n8, g, wq, f, true, k_pass<r0, n8, g, wq, f, true>}
+#define R8V(r0, n8, g, wq, f)                                                                        \
+    {r0, n8, g, wq, f, false, false, k_pass<r0, n8, g, wq, f, false, false>},                        \
+        {r0, n8, g, wq, f, true, false, k_pass<r0, n8, g, wq, f, true, false>},                      \
+        {r0, n8, g, wq, f, false, true, k_pass<r0, n8, g, wq, f, false, true>},                      \
+        {r0, n8, g, wq, f, true, true, k_pass<r0, n8, g, wq, f, true, true>}
 static const Variant k_variants[] = {
     /* first passes (B == 1): WQ = 1, G = WM */
     R8V(4, 3, 1, 1, true), R8V(4, 3, 2, 1, true), R8V(4, 3, 4, 1, true),
@@ -248,10 +282,12 @@ static const Variant k_variants[] = {
 };
 #undef R8V
 
-inline const Variant *find(int r0, int n8, int G, int WQ, bool first, bool split = false)
+inline const Variant *find(int r0, int n8, int G, int WQ, bool first, bool split = false, bool hook = false)
 {
     for (const Variant &v : k_variants)
-        if (v.r0 == r0 && v.n8 == n8 && v.G == G && v.WQ == WQ && v.first == first && v.split == split) return &v;
+        if (v.r0 == r0 && v.n8 == n8 && v.G == G && v.WQ == WQ && v.first == first && v.split == split &&
+            v.hook == hook)
+            return &v;
     return nullptr;
 }
 
@@ -271,7 +307,8 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     int n8 = p->nst - 1;
     const bool first = p->B == 1;
     const bool split = split_mode(first) && p->nst > 1;
-    const Variant *v = find(p->radix[0], n8, p->G, p->Wq, first, split);
+    const bool hook = l->load_op != HS_LOAD_PLAIN || l->store_op != HS_STORE_PLAIN;
+    const Variant *v = find(p->radix[0], n8, p->G, p->Wq, first, split, hook);
     for (int s = 1; s < p->nst; s++)
         if (p->radix[s] != 8) v = nullptr;
     if (!v || (first && !p->leaf) || p->Wm * p->Wq != p->G) {
@@ -305,6 +342,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     a.xcd_groups = xcd;
     a.tile_major = first ? (order & 1) : ((order >> 1) & 1);
     a.batch = l->batch;
+    a.dev_twq = getenv("HSFFT_DEV_TWQ") ? atoi(getenv("HSFFT_DEV_TWQ")) : 0;
     const long long tm = (p->A + p->Wm - 1) / p->Wm, tq = (p->B + p->Wq - 1) / p->Wq;
     a.tiles_q = tq;
     a.tiles = tm * tq;
