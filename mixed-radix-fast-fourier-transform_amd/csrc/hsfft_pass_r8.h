@@ -68,6 +68,35 @@ __device__ __forceinline__ void load_tw(double2 (&w)[7], const Args &a, int jt, 
     }
 }
 
+/* Coalesced twiddle staging for radix-8 stages with LLOC >= 8 in tiles of 8 q-columns
+ * (G == WQ == 8): the 8 lanes of kloc-row r of a wave need the contiguous run
+ * tw[L-1 + 7*(q0 + B*kloc) + 0..55]; lane l loads entries (l&7) + 8j (8 cache lines per
+ * instruction instead of ~56 for the per-lane gather), then the run is redistributed
+ * through the wave's own 7 KiB of the (idle) LDS image so that lane (g, r) gets entries
+ * 7g..7g+6. */
+template <int LLOC>
+__device__ __forceinline__ void load_tw_co(double2 (&w)[7], const Args &a, int jt, long long q0)
+{
+    const int lane = threadIdx.x & 63;
+    const int kloc = jt & (LLOC - 1); /* lane (g, jt): jt is the run's row, g picks entries */
+    const long long base = a.B * LLOC - 1 + 7 * (q0 + a.B * kloc);
+#pragma unroll
+    for (int j = 0; j < 7; j++) w[j] = a.tw[base + (lane & 7) + 8 * j];
+}
+
+__device__ __forceinline__ void redistribute_tw(double2 (&w)[7], double2 *lds)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double2 *reg = lds + wave * 448 + (lane >> 3) * 56;
+#pragma unroll
+    for (int j = 0; j < 7; j++) reg[(lane & 7) + 8 * j] = w[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = reg[(lane & 7) * 7 + i];
+}
+
 /* apply the stage's twiddles (unless this is the leaf) and the 8/R butterflies */
 template <int R, int LLOC, int TPG>
 __device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const double2 (&w)[7], const Args &a,
@@ -217,22 +246,40 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
             }
     }
 
+    /* twiddles are loaded one stage ahead; CTW stages load coalesced runs and redistribute
+     * them through the LDS image right after the exchange that precedes their use */
+    constexpr bool CTW = !FIRST && G == 8 && WQ == 8 && !SPLIT && P * G >= 8 * (TPG * G / 64) * 56;
+    const long long q0 = q - g % WQ;
     double2 wa[7], wb[7];
     if constexpr (!FIRST) load_tw<R0, 1, TPG>(wa, a, jt, q, valid);
-    if constexpr (N8 >= 1) load_tw<8, S::Lloc(1), TPG>(wb, a, jt, q, valid);
+    if constexpr (N8 >= 1) {
+        if constexpr (CTW) load_tw_co<S::Lloc(1)>(wb, a, jt, q0);
+        else load_tw<8, S::Lloc(1), TPG>(wb, a, jt, q, valid);
+    }
     do_stage<R0, 1, TPG>(xr, xi, wa, a, jt, q, FIRST);
     if constexpr (N8 >= 1) {
-        if constexpr (N8 >= 2) load_tw<8, S::Lloc(2), TPG>(wa, a, jt, q, valid);
+        if constexpr (N8 >= 2) {
+            if constexpr (CTW) load_tw_co<S::Lloc(2)>(wa, a, jt, q0);
+            else load_tw<8, S::Lloc(2), TPG>(wa, a, jt, q, valid);
+        }
         exchange<R0, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+        if constexpr (CTW) redistribute_tw(wb, lds);
         do_stage<8, S::Lloc(1), TPG>(xr, xi, wb, a, jt, q, false);
     }
     if constexpr (N8 >= 2) {
-        if constexpr (N8 >= 3) load_tw<8, S::Lloc(3), TPG>(wb, a, jt, q, valid);
+        if constexpr (N8 >= 3) {
+            if constexpr (CTW) load_tw_co<S::Lloc(3)>(wb, a, jt, q0);
+            else load_tw<8, S::Lloc(3), TPG>(wb, a, jt, q, valid);
+        }
+        if constexpr (CTW) __syncthreads(); /* every wave has read its twiddles back */
         exchange<8, S::Lloc(1), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+        if constexpr (CTW) redistribute_tw(wa, lds);
         do_stage<8, S::Lloc(2), TPG>(xr, xi, wa, a, jt, q, false);
     }
     if constexpr (N8 >= 3) {
+        if constexpr (CTW) __syncthreads();
         exchange<8, S::Lloc(2), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+        if constexpr (CTW) redistribute_tw(wb, lds);
         do_stage<8, S::Lloc(3), TPG>(xr, xi, wb, a, jt, q, false);
     }
 
@@ -247,6 +294,61 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
             const long long n = (m * P + kloc + jj * LL) * a.B + q;
             if constexpr (HOOK) store_hook(a, out, n, xr[c * RL + jj], xi[c * RL + jj]);
             else out[n] = make_double2(xr[c * RL + jj], xi[c * RL + jj]);
+        }
+    }
+}
+
+/* Later-pass variant for [8,8,8] (P = 512) tiles of 8 q-columns that transforms T
+ * consecutive rows with the same tile: the twiddles of all three stages are loaded (and
+ * for stages 1-2 redistributed through LDS) once and reused T times, dividing the pass's
+ * twiddle traffic -- for 2^20's pass B about as many bytes as the data itself -- by T. */
+template <int T>
+__global__ __launch_bounds__(512, 4) void k_pass_b512(Args a)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    unsigned blk = blockIdx.x;
+    if (a.xcd_groups > 0) {
+        const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blk % 8;
+        blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blk / 8;
+    }
+    const unsigned tiles = (unsigned)a.tiles;
+    const unsigned bg = blk / tiles, tile = blk % tiles;
+    const int tid = threadIdx.x, g = tid % G, jt = tid / G;
+    const long long q0 = (long long)tile * G, q = q0 + g;
+    /* stage-2 twiddles (the 14 MiB table) loaded coalesced once and kept in registers for
+     * all T rows; stage 0/1 (0.2 / 1.8 MiB tables, cache-resident) are reloaded per row */
+    double2 w2[7];
+    load_tw_co<64>(w2, a, jt, q0);
+    redistribute_tw(w2, lds);
+    __syncthreads();
+    const unsigned b0 = bg * T;
+#pragma unroll 1
+    for (int it = 0; it < T; it++) {
+        const unsigned b = b0 + it;
+        if (b >= (unsigned)a.batch) break;
+        const double2 *in = a.in + (long long)b * a.idist;
+        double2 *out = a.out + (long long)b * a.odist;
+        double xr[8], xi[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const double2 v = in[(long long)(jt + i * TPG) * a.B + q];
+            xr[i] = v.x;
+            xi[i] = v.y;
+        }
+        double2 w[7];
+        load_tw<8, 1, TPG>(w, a, jt, q, true);
+        do_stage<8, 1, TPG>(xr, xi, w, a, jt, q, false);
+        load_tw<8, 8, TPG>(w, a, jt, q, true);
+        exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+        do_stage<8, 8, TPG>(xr, xi, w, a, jt, q, false);
+        exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+        do_stage<8, 64, TPG>(xr, xi, w2, a, jt, q, false);
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const long long n = (long long)(jt + jj * 64) * a.B + q;
+            if (a.store_op == HS_STORE_PLAIN) out[n] = make_double2(xr[jj], xi[jj]);
+            else store_hook(a, out, n, xr[jj], xi[jj]);
         }
     }
 }
@@ -308,6 +410,39 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     const bool first = p->B == 1;
     const bool split = split_mode(first) && p->nst > 1;
     const bool hook = l->load_op != HS_LOAD_PLAIN || l->store_op != HS_STORE_PLAIN;
+    static int tloop = -1;
+    if (tloop < 0) {
+        const char *e = getenv("HSFFT_BLOOP");
+        tloop = e ? atoi(e) : 4;
+    }
+    if (!first && p->nst == 3 && p->radix[0] == 8 && p->G == 8 && p->Wq == 8 && p->A == 1 && p->B % 8 == 0 &&
+        l->load_op == HS_LOAD_PLAIN && tloop > 1 && l->batch >= 2) {
+        kfn fn = tloop >= 8 ? (kfn)k_pass_b512<8> : tloop >= 4 ? (kfn)k_pass_b512<4> : (kfn)k_pass_b512<2>;
+        const int T = tloop >= 8 ? 8 : tloop >= 4 ? 4 : 2;
+        Args a;
+        memset(&a, 0, sizeof a);
+        a.in = (const double2 *)l->in;
+        a.out = (double2 *)l->out;
+        a.tw = (const double2 *)l->tw;
+        a.saux = (const double2 *)l->store_aux;
+        a.idist = l->idist;
+        a.odist = l->odist;
+        a.A = 1;
+        a.B = p->B;
+        a.nsig = l->nsig;
+        a.sgn = l->sgn;
+        a.dir = l->dir;
+        a.conj = l->conj;
+        a.store_op = l->store_op;
+        a.xcd_groups = 1;
+        a.batch = l->batch;
+        a.tiles = p->B / 8;
+        a.tiles_q = a.tiles;
+        const long long grid = a.tiles * ((l->batch + T - 1) / T);
+        hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), 512 * 8 * sizeof(double2), st, a);
+        HCHK(hipGetLastError());
+        return 0;
+    }
     const Variant *v = find(p->radix[0], n8, p->G, p->Wq, first, split, hook);
     for (int s = 1; s < p->nst; s++)
         if (p->radix[s] != 8) v = nullptr;
