@@ -71,16 +71,21 @@ class Comm:
 
 def cpu_baseline(cfg, seconds_target=15.0):
     """The reference (oracle/_ref, compiled from the unmodified sources) timed on host cores
-    over a bounded sample; falls back to the oracle restatement ('port') if absent."""
+    over a bounded sample: `sample` distinct transforms, swept `reps` times so that the timed
+    region is ~seconds_target of wall time.  Falls back to the oracle restatement ('port')
+    when the reference build is absent."""
     kind, n, _, seed, _ = cfg
     threads = max(1, min(16, os.cpu_count() or 1))
     ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
     sample = {("c2c", 1 << 20): 128, ("c2c", 12600): 8192, ("c2c", 99991): 64, ("r2c", 1 << 22): 32}.get((kind, n), 64)
     if os.path.exists(ref_so):
         L = ctypes.CDLL(ref_so)
-        L.hsref_time_batch.restype = ctypes.c_double
-        L.hsref_time_batch.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64]
-        secs = L.hsref_time_batch(n, 1, 1 if kind == "r2c" else 0, sample, threads, seed)
+        L.hsref_time_batch_reps.restype = ctypes.c_double
+        L.hsref_time_batch_reps.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, ctypes.c_int]
+        real = 1 if kind == "r2c" else 0
+        t1 = L.hsref_time_batch_reps(n, 1, real, sample, threads, seed, 1)  # calibration sweep
+        reps = max(1, min(1000, int(seconds_target / max(t1, 1e-6))))
+        secs = L.hsref_time_batch_reps(n, 1, real, sample, threads, seed, reps)
         src = "reference"
     else:
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -90,35 +95,42 @@ def cpu_baseline(cfg, seconds_target=15.0):
         lib = T.oracle()
         if kind == "r2c":
             x = T.real_input(n, seed, batch=sample).reshape(sample, n)
-            rp = lib.orc_real_create(n, 1, 0)
+            h = lib.orc_real_create(n, 1, 0)
             y = np.zeros((sample, n), dtype=np.complex128)
-            t0 = time.perf_counter()
-            lib.orc_r2c_batch(rp, T.ptr(x), T.ptr(y), sample, threads)
-            secs = time.perf_counter() - t0
-            lib.orc_real_destroy(rp)
+            go = lambda: lib.orc_r2c_batch(h, T.ptr(x), T.ptr(y), sample, threads)  # noqa: E731
         else:
             x = T.complex_input(n, seed, batch=sample).reshape(sample, n)
-            p = lib.orc_plan_create(n, 1, 0)
+            h = lib.orc_plan_create(n, 1, 0)
             y = np.zeros_like(x)
-            t0 = time.perf_counter()
-            lib.orc_exec_batch(p, T.ptr(x), T.ptr(y), sample, threads)
-            secs = time.perf_counter() - t0
-            lib.orc_plan_destroy(p)
+            go = lambda: lib.orc_exec_batch(h, T.ptr(x), T.ptr(y), sample, threads)  # noqa: E731
+        t0 = time.perf_counter()
+        go()
+        t1 = time.perf_counter() - t0
+        reps = max(1, min(1000, int(seconds_target / max(t1, 1e-6))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            go()
+        secs = time.perf_counter() - t0
+        (lib.orc_real_destroy if kind == "r2c" else lib.orc_plan_destroy)(h)
         src = "port"
-    return {"value": round(n * sample / secs / 1e9, 6), "unit": "GSamples/s", "cores": threads, "kind": src,
-            "sample": f"{sample} transforms of N={n} ({kind}), {threads} threads, one plan per thread, "
-                      f"{secs:.2f} s wall"}
+    return {"value": round(n * sample * reps / secs / 1e9, 6), "unit": "GSamples/s", "cores": threads, "kind": src,
+            "sample": f"{sample} distinct transforms of N={n} ({kind}) x {reps} sweeps, {threads} threads, "
+                      f"one plan per thread, {secs:.2f} s wall"}
 
 
-def read_traffic(cfg_name):
+def read_traffic(cfg_name, batch):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
-    FETCH_SIZE x2 [gfx950 calibration] + WRITE_SIZE, per MI355X_MICROARCH.md §HBM)."""
+    FETCH_SIZE x2 [gfx950 calibration] + WRITE_SIZE, per MI355X_MICROARCH.md §HBM), valid only
+    for the batch it was measured at."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(cfg_name)
+            ent = json.load(f).get(cfg_name)
     except (OSError, ValueError):
         return None
+    if not ent or ent.get("batch", CONFIGS[cfg_name][2]) != batch:
+        return None
+    return ent.get("hbm_bytes_per_launch")
 
 
 def main():
@@ -144,6 +156,7 @@ def main():
     if args.batch:
         batch = args.batch
     samples = n * batch
+    chunk = batch
     if kind == "c2c":
         plan = hsfft.Plan(n, 1)
         din = hsfft.DeviceBuffer(samples * 16)
@@ -154,10 +167,19 @@ def main():
         dtype = "f64 (complex128)"
     else:
         plan = hsfft.RealPlan(n, 1)
+        # the whole per-GPU input stays resident (4096 x 2^22 x 8 B = 128 GiB); the mirrored
+        # N-bin output (16 B per real sample) of all rows would not fit next to it in 288 GB,
+        # so the step writes it chunk by chunk into one output buffer a consumer would drain
+        chunk = min(batch, max(1, (64 << 30) // (n * 16)))
         din = hsfft.DeviceBuffer(samples * 8)
-        dout = hsfft.DeviceBuffer(samples * 16)
+        dout = hsfft.DeviceBuffer(chunk * n * 16)
         hsfft.fill_real(din, samples, seed, rank * samples)
-        run = lambda: hsfft.r2c_batched(plan, din, dout, batch)  # noqa: E731
+
+        def run():
+            for c0 in range(0, batch, chunk):
+                cb = min(chunk, batch - c0)
+                hsfft.check(hsfft.lib().hsfft_r2c_batched(plan.ptr, ctypes.c_void_p(din.ptr + c0 * n * 8),
+                                                          ctypes.c_void_p(dout.ptr), cb), "r2c_batched")
         bytes_per_sample = 24  # read 8 B + write 16 B of the mirrored output
         dtype = "f64"
     hsfft.synchronize()
@@ -182,9 +204,9 @@ def main():
     if kind == "c2c":
         ev_ms, pms = hsfft.time_batched(plan, din, dout, batch, max(1, args.steps))
         npass = plan.num_passes()
-        pass_ms = [p for p in pms[:npass] if p >= 0]
+        pass_ms = [p for p in pms[:npass] if p > 0]
     else:
-        ev_ms = hsfft.time_r2c_batched(plan, din, dout, batch, max(1, args.steps))
+        ev_ms = hsfft.time_r2c_batched(plan, din, dout, chunk, max(1, args.steps)) * (batch / chunk)
     ev_step_ms = comm.max(ev_ms / max(1, args.steps))
 
     ms_per_step = wall / args.steps * 1e3
@@ -204,7 +226,8 @@ def main():
         "dtype": dtype,
         "data": "synthetic (splitmix64 uniform [-1,1), generated in HBM)",
         "config": {"workload": desc, "N": n, "per_gpu_batch": batch, "global_batch": batch * ws,
-                   "parallelism": f"batch-sharded x{ws} (no collective)", "passes": npass},
+                   "parallelism": f"batch-sharded x{ws} (no collective)", "passes": npass,
+                   **({"output_chunk_rows": chunk} if chunk != batch else {})},
         "achieved_hbm_gbs": round(samples * bytes_per_sample * ws / (ms_per_step / 1e3) / 1e9, 1),
         "event_ms_per_step": round(ev_step_ms, 4),
     }
@@ -212,12 +235,12 @@ def main():
         dom = max(range(len(pass_ms)), key=lambda i: pass_ms[i])
         ach = samples * bytes_per_sample / (pass_ms[dom] / 1e3) / 1e9
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config),
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
                            "kernel": f"pass {dom} of {npass}", "pass_ms": [round(p, 4) for p in pass_ms]}
     else:
         ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config),
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
                            "kernel": "whole step (event timed)"}
     # practical HBM ceiling on this device: a 16-B-per-lane stream copy of the same buffers
     nbytes = min(din.nbytes, dout.nbytes) // 16 * 16

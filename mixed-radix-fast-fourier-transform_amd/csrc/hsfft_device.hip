@@ -374,6 +374,7 @@ int grid_for(long long n, int threads)
 }  // namespace
 
 #include "hsfft_pass_r8.h"
+#include "hsfft_pass_mr.h"
 
 extern "C" {
 
@@ -494,6 +495,8 @@ const char *hsd_errstr(void) { return g_err; }
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
 {
     if (p->variant == HS_KV_R8X3) return r8::launch(p, l, stream());
+    if (p->variant == HS_KV_MR && l->load_op == HS_LOAD_PLAIN && l->store_op == HS_STORE_PLAIN)
+        return mr::launch(p, l, stream());
     KArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)l->in;
@@ -543,6 +546,12 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
 }
 
 int r8_has_variant(int r0, int n8, int G, int Wq, int first) { return r8::find(r0, n8, G, Wq, first != 0) != nullptr; }
+
+int mr_has_variant(const hsd_pass *p)
+{
+    hsd_pass tmp = *p;
+    return mr::select(&tmp) != nullptr;
+}
 
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset)
 {

@@ -144,7 +144,7 @@ static int build_passes_pow2(hs_entry *e)
             /* WM columns per workgroup: as many as the LDS (<=128 KiB) and the variant table allow */
             static const int gopts[] = {32, 16, 8, 4, 2, 1};
             int gmax = env_int("HSFFT_G1", 0);
-            if (gmax <= 0) gmax = p->P >= 2048 ? 4 : p->P >= 1024 ? 4 : p->P >= 512 ? 8 : p->P >= 64 ? 16 : 32;
+            if (gmax <= 0) gmax = p->P >= 2048 ? 2 : p->P >= 1024 ? 4 : p->P >= 512 ? 8 : p->P >= 64 ? 16 : 32;
             int G = 1;
             for (unsigned i = 0; i < sizeof gopts / sizeof gopts[0]; i++)
                 if (gopts[i] <= gmax && gopts[i] <= p->A && r8_has_variant(p->radix[0], p->nst - 1, gopts[i], 1, 1)) {
@@ -210,6 +210,7 @@ static int build_passes(hs_entry *e)
         p->Wm = wm;
         p->G = wq * wm;
         p->variant = HS_KV_GENERIC;
+        if (!env_int("HSFFT_GENERIC", 0) && mr_has_variant(p)) p->variant = HS_KV_MR;
         B *= p->P;
         np++;
     }

@@ -28,6 +28,7 @@ extern "C" {
 /* kernel variants */
 #define HS_KV_GENERIC 0   /* runtime radix list, LDS ping-pong */
 #define HS_KV_R8X3 1      /* specialised: 8*8*8 or tails, register butterflies */
+#define HS_KV_MR 2        /* specialised mixed radix list (hsfft_pass_mr.h), else generic */
 
 /* load / store hooks of a pass (Bluestein fusion) */
 #define HS_LOAD_PLAIN 0
@@ -85,6 +86,7 @@ const char *hsd_errstr(void);
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l);
 /* 1 if the register kernel has an instantiation for [r0, 8^n8] with this tile */
 int r8_has_variant(int r0, int n8, int G, int Wq, int first);
+int mr_has_variant(const hsd_pass *p); /* hsfft_pass_mr.h has a kernel for this pass */
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset);
 int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset);
 /* r2c split (real.c:108-132): Z rows of h complex -> X rows of 2h complex */

@@ -1,0 +1,259 @@
+/*
+ * hsfft_pass_mr.h -- register-resident Stockham passes for mixed radix lists (radix 2, 3,
+ * 4, 5, 7, 8 in any order, up to four stages per pass), e.g. 12600 = [3,3,5,5] + [7,8].
+ *
+ * Same data model as hsfft_pass_r8.h (a pass of P points at L = B views its input as
+ * [t][m][q] and writes [m][u][q]; twiddles tw[L-1 + (R-1)k + i-1], k = q + B*kloc; ref
+ * src/highSpeedFFT.c:731-741 and the per-radix combine loops :776-1561), but the radices
+ * are template parameters, so every stage is unrolled with compile-time index math:
+ *  - a column's P points are held by TPG threads; at a stage of radix R the P/R butterflies
+ *    are dealt round-robin (butterfly b = jt + c*TPG), so a thread owns ceil(P/(R*TPG))
+ *    butterflies -- stages whose count does not divide evenly leave some lanes idle;
+ *  - stage-0 inputs come straight from global memory (clamped, unconditional loads), the
+ *    stages exchange through one LDS image of P*G points, the last stage stores to global;
+ *  - G columns per workgroup (consecutive m for first passes, consecutive q for later
+ *    passes: G*16 contiguous bytes per row of the tile).
+ * Included by hsfft_device.hip only.
+ */
+#pragma once
+
+namespace mr {
+
+template <int NST, int R0, int R1, int R2, int R3>
+struct List {
+    static constexpr int R(int s) { return s == 0 ? R0 : s == 1 ? R1 : s == 2 ? R2 : R3; }
+    static constexpr int P = R0 * (NST > 1 ? R1 : 1) * (NST > 2 ? R2 : 1) * (NST > 3 ? R3 : 1);
+    static constexpr int Lloc(int s)
+    {
+        return (s > 0 ? R0 : 1) * (s > 1 ? R1 : 1) * (s > 2 ? R2 : 1);
+    }
+};
+
+struct MArgs {
+    const double2 *in;
+    double2 *out;
+    const double2 *tw;
+    long long idist, odist;
+    int A, B, tiles_q, tiles, batch;
+    int sgn, conj;
+};
+
+constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+/* register slots per thread: the largest NB*R over the pass's stages */
+template <int NST, int R0, int R1, int R2, int R3, int TPG>
+constexpr int nmax()
+{
+    constexpr int P = List<NST, R0, R1, R2, R3>::P;
+    int n = 0;
+    for (int s = 0; s < NST; s++) {
+        const int r = List<NST, R0, R1, R2, R3>::R(s), v = cdiv(P / r, TPG) * r;
+        n = v > n ? v : n;
+    }
+    return n;
+}
+
+/* butterflies of one stage for this thread; x holds NB*R points (butterfly c at c*R) */
+template <int R, int LLOC, int P, int TPG, bool LEAF>
+__device__ __forceinline__ void stage(double *xr, double *xi, const MArgs &a, int jt, int q, bool valid)
+{
+    constexpr int NBF = P / R, NB = cdiv(NBF, TPG);
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        const int b = c * TPG + jt;
+        if (NB * TPG != NBF && b >= NBF) continue; /* idle slot of an uneven stage */
+        if constexpr (!LEAF) {
+            const int kloc = b % LLOC;
+            const long long L = (long long)a.B * LLOC;
+            const long long k = valid ? q + (long long)a.B * kloc : 0;
+            /* radix 4/5/7 combine loops start at k = 1 (ref :826, :904, :1062); 2, 3, 8 do not */
+            const bool skip = (R == 4 || R == 5 || R == 7) && k == 0;
+            if (!skip) {
+                const double2 *w = a.tw + (L - 1 + (long long)(R - 1) * k);
+                double2 t[R - 1];
+#pragma unroll
+                for (int i = 1; i < R; i++) t[i - 1] = w[i - 1];
+#pragma unroll
+                for (int i = 1; i < R; i++)
+                    hsb::twmul(xr[c * R + i], xi[c * R + i], t[i - 1].x, a.conj ? -t[i - 1].y : t[i - 1].y);
+            }
+        }
+        hsb::bfly<R>(&xr[c * R], &xi[c * R], a.sgn, LEAF);
+    }
+}
+
+/* outputs of a stage (radix R, local L) -> LDS -> inputs of the next stage (radix R2) */
+template <int R, int LLOC, int R2, int P, int TPG, int G>
+__device__ __forceinline__ void exchange(double *xr, double *xi, double2 *lds, int jt, int g)
+{
+    constexpr int NBF = P / R, NB = cdiv(NBF, TPG);
+    constexpr int L2 = LLOC * R, NBF2 = P / R2, NB2 = cdiv(NBF2, TPG), S2 = P / (L2 * R2);
+    __syncthreads(); /* the previous exchange's reads are done */
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        const int b = c * TPG + jt;
+        if (NB * TPG != NBF && b >= NBF) continue;
+        const int ml = b / LLOC, kloc = b % LLOC;
+#pragma unroll
+        for (int jj = 0; jj < R; jj++)
+            lds[(ml * LLOC * R + kloc + jj * LLOC) * G + g] = make_double2(xr[c * R + jj], xi[c * R + jj]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NB2; c++) {
+        int b = c * TPG + jt;
+        if (NB2 * TPG != NBF2 && b >= NBF2) b = NBF2 - 1; /* idle slot: read something valid */
+        const int ml = b / L2, kloc = b % L2;
+#pragma unroll
+        for (int i = 0; i < R2; i++) {
+            const double2 v = lds[((ml + i * S2) * L2 + kloc) * G + g];
+            xr[c * R2 + i] = v.x;
+            xi[c * R2 + i] = v.y;
+        }
+    }
+}
+
+template <int NST, int R0, int R1, int R2, int R3, int TPG, int G, bool FIRST, bool LEAF>
+__global__ __launch_bounds__(TPG * G) void k_pass(MArgs a)
+{
+    using LS = List<NST, R0, R1, R2, R3>;
+    constexpr int P = LS::P;
+    constexpr int NM = nmax<NST, R0, R1, R2, R3, TPG>();
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+
+    const unsigned blk = blockIdx.x, tiles = (unsigned)a.tiles;
+    const unsigned b = blk / tiles, tile = blk % tiles;
+    const int tid = threadIdx.x, g = tid % G, jt = tid / G;
+    /* first passes (B == 1): G consecutive m; later passes (A == 1): G consecutive q */
+    const int m = FIRST ? (int)tile * G + g : 0;
+    const int q = FIRST ? 0 : (int)tile * G + g;
+    const bool valid = FIRST ? m < a.A : q < a.B;
+    const double2 *in = a.in + (long long)b * a.idist;
+    double2 *out = a.out + (long long)b * a.odist;
+
+    double xr[NM], xi[NM];
+    {
+        constexpr int NBF = P / R0, NB = cdiv(NBF, TPG);
+#pragma unroll
+        for (int c = 0; c < NB; c++) {
+            int bf = c * TPG + jt;
+            if (NB * TPG != NBF && bf >= NBF) bf = NBF - 1;
+#pragma unroll
+            for (int i = 0; i < R0; i++) {
+                const long long t = bf + i * NBF;
+                const long long n = valid ? (t * a.A + m) * a.B + q : 0;
+                const double2 v = in[n];
+                xr[c * R0 + i] = v.x;
+                xi[c * R0 + i] = v.y;
+            }
+        }
+    }
+    stage<R0, 1, P, TPG, LEAF>(xr, xi, a, jt, q, valid);
+    if constexpr (NST > 1) {
+        exchange<R0, 1, R1, P, TPG, G>(xr, xi, lds, jt, g);
+        stage<R1, LS::Lloc(1), P, TPG, false>(xr, xi, a, jt, q, valid);
+    }
+    if constexpr (NST > 2) {
+        exchange<R1, LS::Lloc(1), R2, P, TPG, G>(xr, xi, lds, jt, g);
+        stage<R2, LS::Lloc(2), P, TPG, false>(xr, xi, a, jt, q, valid);
+    }
+    if constexpr (NST > 3) {
+        exchange<R2, LS::Lloc(2), R3, P, TPG, G>(xr, xi, lds, jt, g);
+        stage<R3, LS::Lloc(3), P, TPG, false>(xr, xi, a, jt, q, valid);
+    }
+    /* last stage: butterfly b = kloc (ml == 0), output u = kloc + jj*LL to [m][u][q] */
+    constexpr int RL = LS::R(NST - 1), LL = LS::Lloc(NST - 1), NBFL = P / RL, NBL = cdiv(NBFL, TPG);
+    if (!valid) return;
+#pragma unroll
+    for (int c = 0; c < NBL; c++) {
+        const int kloc = c * TPG + jt;
+        if (NBL * TPG != NBFL && kloc >= NBFL) continue;
+#pragma unroll
+        for (int jj = 0; jj < RL; jj++) {
+            const long long n = ((long long)m * P + kloc + jj * LL) * a.B + q;
+            out[n] = make_double2(xr[c * RL + jj], xi[c * RL + jj]);
+        }
+    }
+}
+
+typedef void (*kfn)(MArgs);
+
+struct Variant {
+    int nst, r[4], tpg, G;
+    bool first, leaf;
+    kfn fn;
+};
+
+#define MRV(n, a, b, c, d, tpg, g, f, l) {n, {a, b, c, d}, tpg, g, f, l, k_pass<n, a, b, c, d, tpg, g, f, l>}
+static const Variant k_variants[] = {
+    /* 12600 = [3,3,5,5] + [7,8] (BASELINE config 3) */
+    MRV(4, 3, 3, 5, 5, 45, 8, true, true),
+    MRV(2, 7, 8, 1, 1, 8, 45, false, false),
+    MRV(2, 7, 8, 1, 1, 8, 15, false, false),
+    MRV(2, 7, 8, 1, 1, 8, 16, false, false),
+};
+#undef MRV
+
+/* picks a variant for a pass of the generic schedule; fills the tile geometry */
+inline const Variant *select(hsd_pass *p)
+{
+    if (p->nst < 1 || p->nst > 4) return nullptr;
+    const bool first = p->B == 1;
+    if (!first && p->A != 1) return nullptr;
+    const Variant *best = nullptr;
+    long long best_waste = -1;
+    for (const Variant &v : k_variants) {
+        if (v.nst != p->nst || v.first != first || v.leaf != (p->leaf != 0)) continue;
+        bool same = true;
+        for (int s = 0; s < p->nst; s++) same &= v.r[s] == p->radix[s];
+        if (!same) continue;
+        const long long ext = first ? p->A : p->B; /* columns the tiles cover */
+        const long long waste = (ext + v.G - 1) / v.G * v.G - ext;
+        if (!best || waste < best_waste) {
+            best = &v;
+            best_waste = waste;
+        }
+    }
+    if (!best) return nullptr;
+    p->G = best->G;
+    p->Wm = first ? best->G : 1;
+    p->Wq = first ? 1 : best->G;
+    return best;
+}
+
+inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
+{
+    hsd_pass tmp = *p;
+    const Variant *v = select(&tmp);
+    if (!v || l->load_op != HS_LOAD_PLAIN || l->store_op != HS_STORE_PLAIN) {
+        snprintf(g_err, sizeof g_err, "mr: no kernel variant for this pass (P=%d)", p->P);
+        return -4;
+    }
+    MArgs a;
+    a.in = (const double2 *)l->in;
+    a.out = (double2 *)l->out;
+    a.tw = (const double2 *)l->tw;
+    a.idist = l->idist;
+    a.odist = l->odist;
+    a.A = (int)p->A;
+    a.B = (int)p->B;
+    a.sgn = l->sgn;
+    a.conj = l->conj;
+    a.batch = l->batch;
+    const long long ext = v->first ? p->A : p->B;
+    a.tiles = (int)((ext + v->G - 1) / v->G);
+    a.tiles_q = v->first ? 1 : a.tiles;
+    const long long grid = (long long)a.tiles * l->batch;
+    const int threads = v->tpg * v->G;
+    const size_t lds = (size_t)p->P * v->G * sizeof(double2);
+    if (grid <= 0 || grid > 0x7fffffffLL || threads > 1024 || lds > 65536 || p->A > 0x7fffffff ||
+        p->B > 0x7fffffff || (long long)p->A * p->B * p->P > 0x7fffffffLL) {
+        snprintf(g_err, sizeof g_err, "mr: bad geometry grid=%lld threads=%d lds=%zu", grid, threads, lds);
+        return -1;
+    }
+    hipLaunchKernelGGL(v->fn, dim3((unsigned)grid), dim3(threads), lds, st, a);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace mr

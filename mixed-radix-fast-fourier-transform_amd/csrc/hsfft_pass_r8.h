@@ -123,6 +123,17 @@ __device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const
 
 /* stage s outputs -> LDS -> stage s+1 inputs.  SPLIT exchanges the real parts, then the
  * imaginary parts, through a P*G-double image (half the LDS, so twice the workgroups per CU). */
+/* LDS slot of point p.  After a leaf stage (LLOC == 1) consecutive butterflies write R
+ * points apart; with fewer than 8 groups per 128-B bank window that is an R-way bank
+ * conflict, so the low bits are XOR-swizzled with the butterfly index (conflict-free
+ * writes, and the reads of the next stage stay contiguous). */
+template <int R, int LLOC, int G>
+__device__ __forceinline__ int lds_slot(int p)
+{
+    if constexpr (LLOC == 1 && G < 8 && R > 1) return p ^ ((p / R) & (R - 1));
+    return p;
+}
+
 template <int R, int LLOC, int R2, int TPG, int P, int G, bool SPLIT>
 __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], double2 *lds, int jt, int g)
 {
@@ -134,7 +145,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
             const int kloc = b & (LLOC - 1), ml = b / LLOC;
 #pragma unroll
             for (int jj = 0; jj < R; jj++) {
-                const int p = ml * LLOC * R + kloc + jj * LLOC;
+                const int p = lds_slot<R, LLOC, G>(ml * LLOC * R + kloc + jj * LLOC);
                 lds[p * G + g] = make_double2(xr[c * R + jj], xi[c * R + jj]);
             }
         }
@@ -145,7 +156,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
             const int kloc = b & (L2 - 1), ml = b / L2;
 #pragma unroll
             for (int i = 0; i < R2; i++) {
-                const int p = (ml + i * S2) * L2 + kloc;
+                const int p = lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc);
                 const double2 v = lds[p * G + g];
                 xr[c * R2 + i] = v.x;
                 xi[c * R2 + i] = v.y;
@@ -162,7 +173,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
                 const int b = c * TPG + jt;
                 const int kloc = b & (LLOC - 1), ml = b / LLOC;
 #pragma unroll
-                for (int jj = 0; jj < R; jj++) ld[(ml * LLOC * R + kloc + jj * LLOC) * G + g] = x[c * R + jj];
+                for (int jj = 0; jj < R; jj++) ld[lds_slot<R, LLOC, G>(ml * LLOC * R + kloc + jj * LLOC) * G + g] = x[c * R + jj];
             }
             __syncthreads();
 #pragma unroll
@@ -170,7 +181,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
                 const int b = c * TPG + jt;
                 const int kloc = b & (L2 - 1), ml = b / L2;
 #pragma unroll
-                for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[((ml + i * S2) * L2 + kloc) * G + g];
+                for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc) * G + g];
             }
             __syncthreads();
         }
@@ -201,8 +212,19 @@ __device__ __forceinline__ void store_hook(const Args &a, double2 *out, long lon
     }
 }
 
+/* waves per SIMD the kernel's LDS footprint allows, capped at 6: asks the register
+ * allocator for at most 512/6 VGPRs when LDS would let a third workgroup in (split
+ * exchange of a 512-thread first pass: 32 KiB per workgroup) */
+template <int R0, int N8, int G, bool FIRST, bool SPLIT>
+constexpr int occ_hint()
+{
+    constexpr int thr = Shape<R0, N8>::TPG * G, lds = Shape<R0, N8>::P * G * (SPLIT ? 8 : 16);
+    constexpr int wg = 163840 / lds, w = wg * (thr / 64) / 4;
+    return FIRST && thr == 512 && w >= 6 ? 6 : 1;
+}
+
 template <int R0, int N8, int G, int WQ, bool FIRST, bool SPLIT, bool HOOK>
-__global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (occ_hint<R0, N8, G, FIRST, SPLIT>())) void k_pass(Args a)
 {
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG, WM = G / WQ;
@@ -251,6 +273,24 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
     constexpr bool CTW = !FIRST && G == 8 && WQ == 8 && !SPLIT && P * G >= 8 * (TPG * G / 64) * 56;
     const long long q0 = q - g % WQ;
     double2 wa[7], wb[7];
+    if constexpr (FIRST) { /* tiny, cache-resident tables: load at use, keep VGPRs low */
+        do_stage<R0, 1, TPG>(xr, xi, wa, a, jt, q, true);
+        if constexpr (N8 >= 1) {
+            exchange<R0, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            load_tw<8, S::Lloc(1), TPG>(wa, a, jt, q, valid);
+            do_stage<8, S::Lloc(1), TPG>(xr, xi, wa, a, jt, q, false);
+        }
+        if constexpr (N8 >= 2) {
+            exchange<8, S::Lloc(1), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            load_tw<8, S::Lloc(2), TPG>(wa, a, jt, q, valid);
+            do_stage<8, S::Lloc(2), TPG>(xr, xi, wa, a, jt, q, false);
+        }
+        if constexpr (N8 >= 3) {
+            exchange<8, S::Lloc(2), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            load_tw<8, S::Lloc(3), TPG>(wa, a, jt, q, valid);
+            do_stage<8, S::Lloc(3), TPG>(xr, xi, wa, a, jt, q, false);
+        }
+    } else {
     if constexpr (!FIRST) load_tw<R0, 1, TPG>(wa, a, jt, q, valid);
     if constexpr (N8 >= 1) {
         if constexpr (CTW) load_tw_co<S::Lloc(1)>(wb, a, jt, q0);
@@ -281,6 +321,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G)) void k_pass(Args a)
         exchange<8, S::Lloc(2), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
         if constexpr (CTW) redistribute_tw(wb, lds);
         do_stage<8, S::Lloc(3), TPG>(xr, xi, wb, a, jt, q, false);
+    }
     }
 
     /* last stage: ml == 0, output u = kloc + jj*LL, written to [m][u][q] */
@@ -398,7 +439,7 @@ inline int split_mode(bool first)
     static int m = -1;
     if (m < 0) {
         const char *e = getenv("HSFFT_SPLIT");
-        m = e ? atoi(e) : 0;
+        m = e ? atoi(e) : 1; /* split exchange for first passes only */
     }
     return first ? (m & 1) : ((m >> 1) & 1);
 }
@@ -413,7 +454,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     static int tloop = -1;
     if (tloop < 0) {
         const char *e = getenv("HSFFT_BLOOP");
-        tloop = e ? atoi(e) : 4;
+        tloop = e ? atoi(e) : 8;
     }
     if (!first && p->nst == 3 && p->radix[0] == 8 && p->G == 8 && p->Wq == 8 && p->A == 1 && p->B % 8 == 0 &&
         l->load_op == HS_LOAD_PLAIN && tloop > 1 && l->batch >= 2) {

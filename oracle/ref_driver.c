@@ -40,7 +40,7 @@ static double now_s(void)
 }
 
 typedef struct {
-    int N, sgn, real, b0, b1;
+    int N, sgn, real, b0, b1, reps;
     uint64_t seed;
     pthread_barrier_t *bar;
     double elapsed;
@@ -61,6 +61,7 @@ static void *rd_worker(void *arg)
     }
     pthread_barrier_wait(j->bar);
     double t0 = now_s();
+    for (int rep = 0; rep < j->reps; rep++)
     for (size_t r = 0; r < rows; r++) {
         if (j->real) fft_r2c_exec(obj, in + r * nin, out + r * (size_t)N);
         else fft_exec(obj, (rd_cplx *)(in + r * nin), out + r * (size_t)N);
@@ -73,20 +74,22 @@ static void *rd_worker(void *arg)
     return NULL;
 }
 
-/* Times `batch` transforms split over `nthreads` threads; returns wall seconds of the
- * slowest thread (plan creation excluded). */
-double hsref_time_batch(int N, int sgn, int real, int batch, int nthreads, uint64_t seed)
+/* Times `reps` sweeps over `batch` distinct transforms split over `nthreads` threads
+ * (batch * reps transforms in all); returns wall seconds of the slowest thread (plan
+ * creation and input generation excluded). */
+double hsref_time_batch_reps(int N, int sgn, int real, int batch, int nthreads, uint64_t seed, int reps)
 {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > batch) nthreads = batch;
     if (nthreads > 512) nthreads = 512;
+    if (reps < 1) reps = 1;
     pthread_t th[512];
     rd_job jobs[512];
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (rd_job){N, sgn, real, (int)((long)batch * t / nthreads),
-                           (int)((long)batch * (t + 1) / nthreads), seed, &bar, 0.0};
+                           (int)((long)batch * (t + 1) / nthreads), reps, seed, &bar, 0.0};
         pthread_create(&th[t], NULL, rd_worker, &jobs[t]);
     }
     double worst = 0.0;
@@ -96,4 +99,9 @@ double hsref_time_batch(int N, int sgn, int real, int batch, int nthreads, uint6
     }
     pthread_barrier_destroy(&bar);
     return worst;
+}
+
+double hsref_time_batch(int N, int sgn, int real, int batch, int nthreads, uint64_t seed)
+{
+    return hsref_time_batch_reps(N, sgn, real, batch, nthreads, seed, 1);
 }
