@@ -547,6 +547,12 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
 
 int r8_has_variant(int r0, int n8, int G, int Wq, int first) { return r8::find(r0, n8, G, Wq, first != 0) != nullptr; }
 
+int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
+                 int conj, int dir, int sgn2, int conj2)
+{
+    return r8::launch_blue_mid(in, out, dist, tw, hk, batch, sgn, conj, dir, sgn2, conj2, stream());
+}
+
 int mr_has_variant(const hsd_pass *p)
 {
     hsd_pass tmp = *p;

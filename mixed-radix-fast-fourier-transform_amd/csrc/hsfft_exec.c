@@ -101,7 +101,9 @@ static int build_passes_pow2(hs_entry *e)
         if (e->stage_r[s] != 8) return -1;
     if (env_int("HSFFT_GENERIC", 0)) return -1;
     int n8 = e->nst - 1;            /* radix-8 stages after stage 0 */
-    const int k1max = r0 == 8 ? 2 : 3; /* P <= 2048 and at most 4 stages per pass */
+    /* at most 4 stages per pass; P <= 2048 unless r0 == 8 and a 4096-point first pass
+     * saves a whole pass (2^21 = [8,8,8,8] + [8,8,8]) */
+    const int k1max = r0 == 8 ? (n8 == 6 ? 3 : 2) : 3;
     /* number of later passes needed if the first takes k1 eights: ceil((n8-k1)/3) */
     int best_k1 = -1, best_np = 1 << 30, best_bal = 1 << 30;
     for (int k1 = r0 == 8 ? 0 : 1; k1 <= k1max && k1 <= n8; k1++) { /* every pass needs P >= 8 */
@@ -144,7 +146,7 @@ static int build_passes_pow2(hs_entry *e)
             /* WM columns per workgroup: as many as the LDS (<=128 KiB) and the variant table allow */
             static const int gopts[] = {32, 16, 8, 4, 2, 1};
             int gmax = env_int("HSFFT_G1", 0);
-            if (gmax <= 0) gmax = p->P >= 2048 ? 2 : p->P >= 1024 ? 4 : p->P >= 512 ? 8 : p->P >= 64 ? 16 : 32;
+            if (gmax <= 0) gmax = p->P >= 4096 ? 1 : p->P >= 2048 ? 2 : p->P >= 1024 ? 4 : p->P >= 512 ? 8 : p->P >= 64 ? 16 : 32;
             int G = 1;
             for (unsigned i = 0; i < sizeof gopts / sizeof gopts[0]; i++)
                 if (gopts[i] <= gmax && gopts[i] <= p->A && r8_has_variant(p->radix[0], p->nst - 1, gopts[i], 1, 1)) {
@@ -402,7 +404,7 @@ void hs_entry_release(const struct fft_set *obj)
 }
 
 /* ------------------------------------------------------------------ scratch */
-#define HS_NSCRATCH 8
+#define HS_NSCRATCH 10
 static void *g_scr[HS_MAX_DEV][HS_NSCRATCH];
 static size_t g_scr_sz[HS_MAX_DEV][HS_NSCRATCH];
 
@@ -601,12 +603,13 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     if (!need && n == 2 && chunk < batch && env_int("HSFFT_PIPE", 0))
         return run_pipelined(e, ds, I, idist, O, odist, batch, (int)chunk, sgn, conj, dir, load_op, laux, store_op,
                              saux, nsig);
+    const int dev_np = env_int("HSFFT_DEV_NPASS", 0); /* dev probe: stop after this many passes */
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         const void *R = (const fft_data *)I + c0 * idist;
         long long rdist = idist;
         int lop = load_op, j = 0;
-        for (int i = 0; i < n; i++) {
+        for (int i = 0; i < (dev_np > 0 && dev_np < n ? dev_np : n); i++) {
             void *W;
             long long wdist;
             if (i == n - 1 || (i == n - 2 && last_inplace)) {
@@ -639,7 +642,28 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
     if (chunk > batch) chunk = batch;
     void *mid = hs_scratch(3, sizeof(fft_data) * (size_t)(chunk * M));
     if (!mid) return HSFFT_ERR_NOMEM;
-    for (long long c0 = 0; c0 < batch; c0 += chunk) {
+    /* M = 512 x 512 as two [8,8,8] passes: the forward FFT's last pass, the spectrum product
+     * and the inverse FFT's first pass run as one kernel (the columns coincide) */
+    const hsd_pass *p0 = &e->pass[0], *p1 = &e->pass[1];
+    const int fuse = e->npass == 2 && M == 512 * 512 && p0->P == 512 && p1->P == 512 && p0->nst == 3 &&
+                     p1->nst == 3 && p0->variant == HS_KV_R8X3 && p1->variant == HS_KV_R8X3 &&
+                     p0->radix[0] == 8 && !env_int("HSFFT_BLUE_NOFUSE", 0);
+    void *mid2 = fuse ? hs_scratch(8, sizeof(fft_data) * (size_t)(chunk * M)) : NULL;
+    if (fuse && !mid2) return HSFFT_ERR_NOMEM;
+    for (long long c0 = 0; c0 < batch && fuse; c0 += chunk) {
+        const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
+        int rc = launch_pass(e, ds, 0, (const fft_data *)in + c0 * idist, idist, mid, M, cb, e->sgn, 0, e->sgn,
+                             HS_LOAD_CHIRP, ds->d_chirp, HS_STORE_PLAIN, NULL, N);
+        if (!rc && hsd_blue_mid(mid, mid2, M, ds->d_tw, ds->d_hk, cb, e->sgn, 0, e->sgn, -1 * e->sgn, 1)) {
+            hs_seterr("bluestein middle: %s", hsd_errstr());
+            rc = HSFFT_ERR_DEVICE;
+        }
+        if (!rc)
+            rc = launch_pass(e, ds, 1, mid2, M, (fft_data *)out + c0 * odist, odist, cb, -1 * e->sgn, 1, e->sgn,
+                             HS_LOAD_PLAIN, NULL, HS_STORE_CHIRP, ds->d_chirp, N);
+        if (rc) return rc;
+    }
+    for (long long c0 = 0; c0 < batch && !fuse; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         int rc = run_chain(e, ds, (const fft_data *)in + c0 * idist, idist, mid, M, cb, e->sgn, 0, e->sgn,
                            HS_LOAD_CHIRP, ds->d_chirp, HS_STORE_SPEC, ds->d_hk, N);

@@ -86,7 +86,10 @@ const char *hsd_errstr(void);
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l);
 /* 1 if the register kernel has an instantiation for [r0, 8^n8] with this tile */
 int r8_has_variant(int r0, int n8, int G, int Wq, int first);
-int mr_has_variant(const hsd_pass *p); /* hsfft_pass_mr.h has a kernel for this pass */
+int mr_has_variant(const hsd_pass *p);
+/* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
+int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
+                 int conj, int dir, int sgn2, int conj2); /* hsfft_pass_mr.h has a kernel for this pass */
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset);
 int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset);
 /* r2c split (real.c:108-132): Z rows of h complex -> X rows of 2h complex */

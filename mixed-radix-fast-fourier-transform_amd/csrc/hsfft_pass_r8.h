@@ -26,7 +26,6 @@ struct Args {
     int xcd_groups;   /* >0: remap block ids so that consecutive tiles share an XCD */
     int tile_major;   /* 1: block order tile-major (all rows of a tile adjacent) */
     long long batch;
-    int dev_twq;      /* development probe only: twiddle column = q (wrong results, timing) */
 };
 
 template <int N>
@@ -61,7 +60,7 @@ __device__ __forceinline__ void load_tw(double2 (&w)[7], const Args &a, int jt, 
         const int kloc = (c * TPG + jt) & (LLOC - 1);
         /* invalid lanes read column 0 (always in range): no branch around the loads, which
          * would make hipcc wait vmcnt(0) after each one */
-        const long long k = valid ? q + (a.dev_twq ? 0 : a.B * kloc) : 0;
+        const long long k = valid ? q + a.B * kloc : 0;
         const double2 *p = a.tw + (L - 1 + (long long)(R - 1) * k);
 #pragma unroll
         for (int i = 1; i < R; i++) w[c * (R - 1) + i - 1] = p[i - 1];
@@ -130,8 +129,21 @@ __device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const
 template <int R, int LLOC, int G>
 __device__ __forceinline__ int lds_slot(int p)
 {
+#ifndef HS_NOSWZ
     if constexpr (LLOC == 1 && G < 8 && R > 1) return p ^ ((p / R) & (R - 1));
+#endif
     return p;
+}
+
+/* Materialise LDS-loaded values before the barrier that follows their loads.  Without it
+ * hipcc (ROCm 7.2) may sink a ds_read whose only uses lie after the barrier to those uses,
+ * i.e. past the barrier: the next exchange's writes from faster waves then race with it
+ * (observed: k_pass<4,3,1,1> / <8,3,1,1> lost whole columns).  The empty asm "uses" each
+ * value where it stands and emits no instruction. */
+__device__ __forceinline__ void pin(double (&x)[8])
+{
+#pragma unroll
+    for (int i = 0; i < 8; i++) asm volatile("" : "+v"(x[i]));
 }
 
 template <int R, int LLOC, int R2, int TPG, int P, int G, bool SPLIT>
@@ -162,6 +174,8 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
                 xi[c * R2 + i] = v.y;
             }
         }
+        pin(xr);
+        pin(xi);
         __syncthreads();
     } else {
         double *ld = reinterpret_cast<double *>(lds);
@@ -183,6 +197,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
 #pragma unroll
                 for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc) * G + g];
             }
+            pin(x);
             __syncthreads();
         }
     }
@@ -394,6 +409,100 @@ __global__ __launch_bounds__(512, 4) void k_pass_b512(Args a)
     }
 }
 
+/* Bluestein middle for M = 512*512 (ref :1797-1855): the last pass of the forward FFT of
+ * the chirped row ([8,8,8] at L = B = 512, tiles of 8 q-columns), the spectrum product with
+ * hk (:1803-1827) and the first pass of the inverse FFT ([8,8,8] leaf, conjugated twiddles,
+ * sign -sgn; :1838-1855) on the same registers: column q of the former is column m = q of
+ * the latter and thread jt holds points u = jt + 64*i of both, so the intermediate never
+ * goes back to HBM.  a.sgn/a.conj: forward FFT; sgn2/conj2: inverse FFT; a.saux = hk. */
+__global__ __launch_bounds__(512) void k_blue_mid(Args a, int sgn2, int conj2)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    unsigned blk = blockIdx.x;
+    {
+        const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blk % 8;
+        blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blk / 8;
+    }
+    const unsigned tiles = (unsigned)a.tiles, b = blk / tiles, tile = blk % tiles;
+    const int tid = threadIdx.x, g = tid % G, jt = tid / G;
+    const long long q0 = (long long)tile * G, q = q0 + g;
+    const double2 *in = a.in + (long long)b * a.idist;
+    double2 *out = a.out + (long long)b * a.odist;
+    double xr[8], xi[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const double2 v = in[(long long)(jt + i * TPG) * a.B + q];
+        xr[i] = v.x;
+        xi[i] = v.y;
+    }
+    /* forward FFT, last pass (twiddles as in k_pass's coalesced later-pass path) */
+    double2 wa[7], wb[7];
+    load_tw<8, 1, TPG>(wa, a, jt, q, true);
+    load_tw_co<8>(wb, a, jt, q0);
+    do_stage<8, 1, TPG>(xr, xi, wa, a, jt, q, false);
+    load_tw_co<64>(wa, a, jt, q0);
+    exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    redistribute_tw(wb, lds);
+    do_stage<8, 8, TPG>(xr, xi, wb, a, jt, q, false);
+    __syncthreads();
+    exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    redistribute_tw(wa, lds);
+    do_stage<8, 64, TPG>(xr, xi, wa, a, jt, q, false);
+    /* spectrum product: element u*B + q, u = jt + 64*jj (store_hook's HS_STORE_SPEC) */
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) {
+        const double2 k = a.saux[(long long)(jt + jj * TPG) * a.B + q];
+        const double yr = xr[jj], yi = xi[jj];
+        if (a.dir == 1) {
+            xr[jj] = yr * k.x - yi * k.y;
+            xi[jj] = yr * k.y + yi * k.x;
+        } else {
+            xr[jj] = yr * k.x + yi * k.y;
+            xi[jj] = -yr * k.y + yi * k.x;
+        }
+    }
+    /* inverse FFT, first pass: column m = q, L = 1 */
+    Args a2 = a;
+    a2.B = 1;
+    a2.sgn = sgn2;
+    a2.conj = conj2;
+    do_stage<8, 1, TPG>(xr, xi, wa, a2, jt, 0, true);
+    __syncthreads(); /* every wave has read its redistributed twiddles */
+    exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    load_tw<8, 8, TPG>(wa, a2, jt, 0, true);
+    do_stage<8, 8, TPG>(xr, xi, wa, a2, jt, 0, false);
+    exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    load_tw<8, 64, TPG>(wa, a2, jt, 0, true);
+    do_stage<8, 64, TPG>(xr, xi, wa, a2, jt, 0, false);
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) out[q * P + jt + jj * TPG] = make_double2(xr[jj], xi[jj]);
+}
+
+inline int launch_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch,
+                           int sgn, int conj, int dir, int sgn2, int conj2, hipStream_t st)
+{
+    Args a;
+    memset(&a, 0, sizeof a);
+    a.in = (const double2 *)in;
+    a.out = (double2 *)out;
+    a.tw = (const double2 *)tw;
+    a.saux = (const double2 *)hk;
+    a.idist = a.odist = dist;
+    a.A = 1;
+    a.B = 512;
+    a.sgn = sgn;
+    a.conj = conj;
+    a.dir = dir;
+    a.batch = batch;
+    a.tiles = a.tiles_q = 512 / 8;
+    const long long grid = a.tiles * (long long)batch;
+    if (grid <= 0 || grid > 0x7fffffffLL) return -1;
+    hipLaunchKernelGGL(k_blue_mid, dim3((unsigned)grid), dim3(512), 512 * 8 * sizeof(double2), st, a, sgn2, conj2);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
 typedef void (*kfn)(Args);
 
 struct Variant {
@@ -411,6 +520,7 @@ static const Variant k_variants[] = {
     /* first passes (B == 1): WQ = 1, G = WM */
     R8V(4, 3, 1, 1, true), R8V(4, 3, 2, 1, true), R8V(4, 3, 4, 1, true),
     R8V(2, 3, 1, 1, true), R8V(2, 3, 2, 1, true), R8V(2, 3, 4, 1, true),
+    R8V(8, 3, 1, 1, true), R8V(8, 3, 2, 1, true),
     R8V(8, 2, 1, 1, true), R8V(8, 2, 2, 1, true), R8V(8, 2, 4, 1, true), R8V(8, 2, 8, 1, true),
     R8V(4, 2, 1, 1, true), R8V(4, 2, 4, 1, true), R8V(4, 2, 8, 1, true),
     R8V(2, 2, 1, 1, true), R8V(2, 2, 4, 1, true), R8V(2, 2, 8, 1, true),
@@ -518,7 +628,6 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     a.xcd_groups = xcd;
     a.tile_major = first ? (order & 1) : ((order >> 1) & 1);
     a.batch = l->batch;
-    a.dev_twq = getenv("HSFFT_DEV_TWQ") ? atoi(getenv("HSFFT_DEV_TWQ")) : 0;
     const long long tm = (p->A + p->Wm - 1) / p->Wm, tq = (p->B + p->Wq - 1) / p->Wq;
     a.tiles_q = tq;
     a.tiles = tm * tq;

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhsfft.so")
+LIB_PATH = os.environ.get("HSFFT_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libhsfft.so")
 
 VP = ctypes.c_void_p
 CI = ctypes.c_int

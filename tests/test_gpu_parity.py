@@ -301,3 +301,16 @@ def test_multi_device_api_single_gpu():
     outs = (ctypes.c_void_p * 1)(dout.ptr)
     assert L.hsfft_exec_multi(p.ptr, ins, outs, batch, 1) == 0
     assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), oracle_rows(x, 1))
+
+@pytest.mark.gpu
+def test_two_pass_2pow21_batched():
+    """2^21 = [8,8,8,8] (4096-point first pass) + [8,8,8]: bit-exact vs the oracle."""
+    n = 1 << 21
+    x = T.complex_input(n, 21, batch=3).reshape(3, n)
+    p = hsfft.Plan(n, 1)
+    assert p.num_passes() == 2
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    hsfft.exec_batched(p, din, dout, 3)
+    y = dout.to_array(np.complex128).reshape(3, n)
+    assert T.bits_equal(y, T.oracle_c2c(x, 1))
