@@ -553,6 +553,12 @@ int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, cons
     return r8::launch_blue_mid(in, out, dist, tw, hk, batch, sgn, conj, dir, sgn2, conj2, stream());
 }
 
+int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
+                 long long B, int batch, int sgn)
+{
+    return r8::launch_r2c_last(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream());
+}
+
 int mr_has_variant(const hsd_pass *p)
 {
     hsd_pass tmp = *p;

@@ -129,9 +129,7 @@ __device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const
 template <int R, int LLOC, int G>
 __device__ __forceinline__ int lds_slot(int p)
 {
-#ifndef HS_NOSWZ
     if constexpr (LLOC == 1 && G < 8 && R > 1) return p ^ ((p / R) & (R - 1));
-#endif
     return p;
 }
 
@@ -409,6 +407,35 @@ __global__ __launch_bounds__(512, 4) void k_pass_b512(Args a)
     }
 }
 
+/* A later [8,8,8] pass (P = 512, A == 1) for the 8 q-columns q0..q0+7 of one row, as in
+ * k_pass's coalesced-twiddle path; on return thread (g, jt) holds outputs u = jt + 64*jj of
+ * column q0 + g.  Starts with a barrier, so it may follow any earlier LDS use. */
+__device__ __forceinline__ void tile888(double (&xr)[8], double (&xi)[8], const Args &a, const double2 *in,
+                                        long long q0, int jt, int g, double2 *lds)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    const long long q = q0 + g;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const double2 v = in[(long long)(jt + i * TPG) * a.B + q];
+        xr[i] = v.x;
+        xi[i] = v.y;
+    }
+    double2 wa[7], wb[7];
+    load_tw<8, 1, TPG>(wa, a, jt, q, true);
+    load_tw_co<8>(wb, a, jt, q0);
+    do_stage<8, 1, TPG>(xr, xi, wa, a, jt, q, false);
+    load_tw_co<64>(wa, a, jt, q0);
+    __syncthreads(); /* earlier LDS readers (redistributed twiddles, exchanges) are done */
+    exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    redistribute_tw(wb, lds);
+    do_stage<8, 8, TPG>(xr, xi, wb, a, jt, q, false);
+    __syncthreads();
+    exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    redistribute_tw(wa, lds);
+    do_stage<8, 64, TPG>(xr, xi, wa, a, jt, q, false);
+}
+
 /* Bluestein middle for M = 512*512 (ref :1797-1855): the last pass of the forward FFT of
  * the chirped row ([8,8,8] at L = B = 512, tiles of 8 q-columns), the spectrum product with
  * hk (:1803-1827) and the first pass of the inverse FFT ([8,8,8] leaf, conjugated twiddles,
@@ -430,25 +457,7 @@ __global__ __launch_bounds__(512) void k_blue_mid(Args a, int sgn2, int conj2)
     const double2 *in = a.in + (long long)b * a.idist;
     double2 *out = a.out + (long long)b * a.odist;
     double xr[8], xi[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const double2 v = in[(long long)(jt + i * TPG) * a.B + q];
-        xr[i] = v.x;
-        xi[i] = v.y;
-    }
-    /* forward FFT, last pass (twiddles as in k_pass's coalesced later-pass path) */
-    double2 wa[7], wb[7];
-    load_tw<8, 1, TPG>(wa, a, jt, q, true);
-    load_tw_co<8>(wb, a, jt, q0);
-    do_stage<8, 1, TPG>(xr, xi, wa, a, jt, q, false);
-    load_tw_co<64>(wa, a, jt, q0);
-    exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
-    redistribute_tw(wb, lds);
-    do_stage<8, 8, TPG>(xr, xi, wb, a, jt, q, false);
-    __syncthreads();
-    exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
-    redistribute_tw(wa, lds);
-    do_stage<8, 64, TPG>(xr, xi, wa, a, jt, q, false);
+    tile888(xr, xi, a, in, q0, jt, g, lds); /* forward FFT, last pass */
     /* spectrum product: element u*B + q, u = jt + 64*jj (store_hook's HS_STORE_SPEC) */
 #pragma unroll
     for (int jj = 0; jj < 8; jj++) {
@@ -467,6 +476,7 @@ __global__ __launch_bounds__(512) void k_blue_mid(Args a, int sgn2, int conj2)
     a2.B = 1;
     a2.sgn = sgn2;
     a2.conj = conj2;
+    double2 wa[7];
     do_stage<8, 1, TPG>(xr, xi, wa, a2, jt, 0, true);
     __syncthreads(); /* every wave has read its redistributed twiddles */
     exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
@@ -499,6 +509,109 @@ inline int launch_blue_mid(const void *in, void *out, long long dist, const void
     const long long grid = a.tiles * (long long)batch;
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     hipLaunchKernelGGL(k_blue_mid, dim3((unsigned)grid), dim3(512), 512 * 8 * sizeof(double2), st, a, sgn2, conj2);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+/* r2c split fused into the last c2c pass (ref real.c:108-132).  For h = N/2 whose c2c plan
+ * ends in a later [8,8,8] pass with A == 1 (columns q < B, B % 16 == 0), output k = u*B + q
+ * of that pass pairs with h - k = (P-1-u)*B + (B-q) (q > 0), so the lo tile of columns
+ * [8j+1, 8j+9) and the hi tile [B-8j-8, B-8j) are closed under the pairing: a workgroup
+ * computes both tiles, swaps the hi tile through LDS, and writes X[k], X[N-k], X[h-k] and
+ * X[h+k] for every k of its lo tile.  Tile j == B/16 handles column 0 (u <-> P-u, X[0], X[h]).
+ * a.in: pass-A output (row dist idist), a.out: X (row dist odist = N), a.saux: twiddle2. */
+__device__ __forceinline__ void r2c_pair(double2 a, double2 c, double2 w, double &re, double &im)
+{
+    const double t1 = a.y + c.y, t2 = c.x - a.x;
+    re = (a.x + c.x + (t1 * w.x) + (t2 * w.y)) / 2.0;
+    im = (a.y - c.y + (t2 * w.x) - (t1 * w.y)) / 2.0;
+}
+
+__global__ __launch_bounds__(512, 4) void k_r2c_last(Args a, long long h)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    unsigned blk = blockIdx.x;
+    {
+        const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blk % 8;
+        blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blk / 8;
+    }
+    const unsigned tiles = (unsigned)a.tiles, b = blk / tiles, j = blk % tiles;
+    const int tid = threadIdx.x, g = tid % G, jt = tid / G;
+    const long long B = a.B, N = 2 * h;
+    const double2 *in = a.in + (long long)b * a.idist;
+    double2 *X = a.out + (long long)b * a.odist;
+    const double2 *w2 = a.saux;
+    double xr[8], xi[8];
+    if (j < tiles - 1) {
+        const long long qlo = 8 * (long long)j + 1, qhi = B - 8 * (long long)j - 8;
+        double hr[8], hi[8];
+        tile888(hr, hi, a, in, qhi, jt, g, lds);
+        tile888(xr, xi, a, in, qlo, jt, g, lds);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(hr[jj], hi[jj]);
+        __syncthreads();
+        const long long q = qlo + g;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const int u = jt + jj * TPG;
+            const long long k = u * B + q, hk = h - k;
+            const double2 zk = make_double2(xr[jj], xi[jj]), zh = lds[(P - 1 - u) * G + (7 - g)];
+            double re, im;
+            r2c_pair(zk, zh, w2[k], re, im);
+            X[k] = make_double2(re, im);
+            X[N - k] = make_double2(re, -im);
+            r2c_pair(zh, zk, w2[hk], re, im);
+            X[hk] = make_double2(re, im);
+            X[N - hk] = make_double2(re, -im);
+        }
+    } else { /* column 0: k = u*B pairs with (P-u)*B */
+        tile888(xr, xi, a, in, 0, jt, g, lds);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const int u = jt + jj * TPG;
+            const long long k = u * B;
+            const double2 zk = make_double2(xr[jj], xi[jj]);
+            if (u == 0) {
+                X[0] = make_double2(zk.x + zk.y, 0.0);
+                X[h] = make_double2(zk.x - zk.y, 0.0);
+            } else {
+                const double2 zh = lds[(P - u) * G];
+                double re, im;
+                r2c_pair(zk, zh, w2[k], re, im);
+                X[k] = make_double2(re, im);
+                X[N - k] = make_double2(re, -im);
+            }
+        }
+    }
+}
+
+inline int launch_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2,
+                           long long h, long long B, int batch, int sgn, hipStream_t st)
+{
+    if (B % 16 || B * 512 != h) return -1;
+    Args a;
+    memset(&a, 0, sizeof a);
+    a.in = (const double2 *)Z;
+    a.out = (double2 *)X;
+    a.tw = (const double2 *)tw;
+    a.saux = (const double2 *)w2;
+    a.idist = zdist;
+    a.odist = xdist;
+    a.A = 1;
+    a.B = B;
+    a.sgn = sgn;
+    a.batch = batch;
+    a.tiles = a.tiles_q = B / 16 + 1;
+    const long long grid = a.tiles * (long long)batch;
+    if (grid <= 0 || grid > 0x7fffffffLL) return -1;
+    hipLaunchKernelGGL(k_r2c_last, dim3((unsigned)grid), dim3(512), 512 * 8 * sizeof(double2), st, a, h);
     HCHK(hipGetLastError());
     return 0;
 }

@@ -103,7 +103,7 @@ void free_real_fft(fft_real_object r)
 static size_t real_chunk_rows(int h)
 {
     const char *s = getenv("HSFFT_CHUNK_MB");
-    size_t bytes = (size_t)(s ? atof(s) : 256.0) * (1u << 20);
+    size_t bytes = (size_t)(s ? atof(s) : 1024.0) * (1u << 20); /* measured: 256 MiB chunks under-fill pass B */
     size_t rows = bytes / (sizeof(fft_data) * (size_t)h);
     return rows ? rows : 1;
 }
@@ -128,8 +128,11 @@ int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, 
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         /* x[2k], x[2k+1] packed as complex = the same bytes (ref real.c:99-103) */
-        rc = hs_c2c_rows(e, d_in + c0 * N, h, Z, h, cb);
-        if (!rc) rc = hsd_r2c_post(Z, tw2, d_out + c0 * N, h, cb, h, N) ? HSFFT_ERR_DEVICE : 0;
+        rc = hs_r2c_fused(e, d_in + c0 * N, h, Z, d_out + c0 * N, N, tw2, cb);
+        if (rc == 1) {
+            rc = hs_c2c_rows(e, d_in + c0 * N, h, Z, h, cb);
+            if (!rc) rc = hsd_r2c_post(Z, tw2, d_out + c0 * N, h, cb, h, N) ? HSFFT_ERR_DEVICE : 0;
+        }
         if (rc) return rc;
     }
     return 0;
