@@ -64,9 +64,59 @@ class Comm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, v):
+        """all ranks' values of a float, in rank order"""
+        if not self.dist:
+            return [v]
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        out = [self.torch.zeros_like(t) for _ in range(self.ws)]
+        self.dist.all_gather(out, t)
+        return [float(x.item()) for x in out]
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
+
+
+def row_range(rank, per_rank_batch):
+    """Weak-scaling shard: rank r transforms global rows [r*B, (r+1)*B) -- the batch index is
+    the only thing split across GPUs (no data-path collective)."""
+    return rank * per_rank_batch, (rank + 1) * per_rank_batch
+
+
+def dry_run(args, comm, ws, rank):
+    """The multi-rank control path without a GPU (CPU tests under gloo): every rank transforms
+    its own rows of a small c2c batch with the CPU oracle, timed with the same barrier /
+    max-over-ranks protocol; rank 0 prints the JSON line plus every rank's row range."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import numpy as np
+
+    import hsfft_testlib as T
+    n, batch = args.dry_n, args.batch or 4
+    r0, r1 = row_range(rank, batch)
+    x = T.complex_input(n, 0x5EED0002, batch=batch, row0=r0).reshape(batch, n)
+    lib = T.oracle()
+    p = lib.orc_plan_create(n, 1, 0)
+    y = np.zeros_like(x)
+    run = lambda: lib.orc_exec_batch(p, T.ptr(x), T.ptr(y), batch, 1)  # noqa: E731
+    for _ in range(args.warmup):
+        run()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    comm.barrier()
+    wall = comm.max(time.perf_counter() - t0)
+    rows = comm.gather(r0)
+    checks = comm.gather(float(np.abs(y).sum()))
+    lib.orc_plan_destroy(p)
+    ms = wall / args.steps * 1e3
+    if rank == 0:
+        print(json.dumps({"metric": f"dry run: c2c N={n} on the CPU oracle (no GPU)", "value": round(
+            n * batch * ws / (ms / 1e3) / 1e9, 6), "unit": "GSamples/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "dry_run": True, "per_rank_batch": batch, "row_starts": [int(r) for r in rows],
+            "rank_checksums": checks}), flush=True)
 
 
 def cpu_baseline(cfg, seconds_target=15.0):
@@ -141,10 +191,16 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch (development only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
+    ap.add_argument("--dry-n", type=int, default=1024)
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
     comm = Comm(ws)
+    if args.dry_run:
+        dry_run(args, comm, ws, rank)
+        comm.close()
+        return
     L = hsfft.lib()
     ndev = hsfft.device_count()
     if ndev < 1:
@@ -161,7 +217,7 @@ def main():
         plan = hsfft.Plan(n, 1)
         din = hsfft.DeviceBuffer(samples * 16)
         dout = hsfft.DeviceBuffer(samples * 16)
-        hsfft.fill_complex(din, samples, seed, rank * samples)
+        hsfft.fill_complex(din, samples, seed, row_range(rank, batch)[0] * n)
         run = lambda: hsfft.exec_batched(plan, din, dout, batch)  # noqa: E731
         bytes_per_sample = 32  # read 16 B + write 16 B
         dtype = "f64 (complex128)"
@@ -173,7 +229,7 @@ def main():
         chunk = min(batch, max(1, (64 << 30) // (n * 16)))
         din = hsfft.DeviceBuffer(samples * 8)
         dout = hsfft.DeviceBuffer(chunk * n * 16)
-        hsfft.fill_real(din, samples, seed, rank * samples)
+        hsfft.fill_real(din, samples, seed, row_range(rank, batch)[0] * n)
 
         def run():
             for c0 in range(0, batch, chunk):

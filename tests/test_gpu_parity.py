@@ -314,3 +314,17 @@ def test_two_pass_2pow21_batched():
     hsfft.exec_batched(p, din, dout, 3)
     y = dout.to_array(np.complex128).reshape(3, n)
     assert T.bits_equal(y, T.oracle_c2c(x, 1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1 << 19, 1 << 22])
+def test_r2c_fused_split_opt_in(n, monkeypatch):
+    """HSFFT_R2C_FUSE=1: the real.c split fused into the last c2c pass (k_r2c_last), bit-exact."""
+    monkeypatch.setenv("HSFFT_R2C_FUSE", "1")
+    x = T.real_input(n, 23, batch=2).reshape(2, n)
+    rp = hsfft.RealPlan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(2 * n * 16)
+    hsfft.r2c_batched(rp, din, dout, 2)
+    y = dout.to_array(np.complex128).reshape(2, n)
+    assert T.bits_equal(y, T.oracle_r2c(x, 1))
