@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hsfft_butterfly.h"
@@ -375,6 +376,8 @@ int grid_for(long long n, int threads)
 
 #include "hsfft_pass_r8.h"
 #include "hsfft_pass_mr.h"
+#include "hsfft_pass_pf.h"
+#include "hsfft_fused.h"
 
 extern "C" {
 
@@ -442,10 +445,138 @@ int hsd_memset_async(void *d, int v, size_t bytes)
     return 0;
 }
 
+/* fused-launch state per device: counter block (heads, error word, per-group counters) and
+ * a pinned host copy of the sticky error word, checked at every synchronisation */
+static unsigned *g_fz_ctr[HS_MAX_DEV];
+static size_t g_fz_bytes[HS_MAX_DEV];
+static unsigned *g_fz_err_host[HS_MAX_DEV];
+
+static int fz_check(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV || !g_fz_err_host[dev]) return 0;
+    if (*(volatile unsigned *)g_fz_err_host[dev] == 0) return 0;
+    *g_fz_err_host[dev] = 0;
+    HCHK(hipMemset(g_fz_ctr[dev] + fz::NQ, 0, sizeof(unsigned)));
+    snprintf(g_err, sizeof g_err, "fused 2^20 launch: a pass-B dependency wait timed out (results invalid)");
+    return -2;
+}
+
 int hsd_sync(void)
 {
     HCHK(hipStreamSynchronize(primary()));
+    return fz_check();
+}
+
+int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
+                int conj, int rows_per_group, int lag, int grid)
+{
+    int dev = 0;
+    HCHK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= HS_MAX_DEV) return -1;
+    const int R = rows_per_group;
+    if ((R != 1 && R != 2 && R != 4) || batch < R || batch % R || (sgn != 1 && sgn != -1) || grid < fz::NQ ||
+        grid % fz::NQ) {
+        snprintf(g_err, sizeof g_err, "hsd_fused20: unsupported geometry (R=%d batch=%d grid=%d)", R, batch, grid);
+        return -1;
+    }
+    const unsigned ng = (unsigned)(batch / R);
+    /* [0, 8): ticket heads, [8]: sticky error word, [12, 12 + ng): group counters; the
+     * per-call memset covers heads + counters only (16-B aligned blocks) */
+    const size_t need = (12 + (size_t)ng) * sizeof(unsigned);
+    if (g_fz_bytes[dev] < need) {
+        if (g_fz_ctr[dev]) {
+            HCHK(hipStreamSynchronize(stream()));
+            HCHK(hipFree(g_fz_ctr[dev]));
+        }
+        const size_t alloc = (need + 4095) & ~(size_t)4095;
+        HCHK(hipMalloc((void **)&g_fz_ctr[dev], alloc));
+        HCHK(hipMemset(g_fz_ctr[dev], 0, alloc));
+        g_fz_bytes[dev] = alloc;
+        if (!g_fz_err_host[dev]) {
+            HCHK(hipHostMalloc((void **)&g_fz_err_host[dev], 64, hipHostMallocDefault));
+            *g_fz_err_host[dev] = 0;
+        }
+    }
+    unsigned *ctr = g_fz_ctr[dev];
+    HCHK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned), stream()));
+    HCHK(hipMemsetAsync(ctr + 12, 0, ((size_t)ng * sizeof(unsigned) + 15) & ~(size_t)15, stream()));
+    fz::FArgs a;
+    a.in = (const double2 *)in;
+    a.out = (double2 *)out;
+    a.tw = (const double2 *)tw;
+    a.idist = idist;
+    a.odist = odist;
+    a.head = ctr;
+    a.err = ctr + 8;
+    a.done = ctr + 12;
+    a.ngroups = ng;
+    a.lag = (unsigned)(lag < 1 ? 1 : lag);
+    {
+        const char *e = getenv("HSFFT_FZ_SPIN");
+        a.spin_max = e ? (unsigned)atoi(e) : (4u << 20);
+    }
+    a.dbg = nullptr;
+    const char *dbgenv = getenv("HSFFT_FZ_DEBUG");
+    static unsigned *s_dbg = nullptr;
+    if (dbgenv && atoi(dbgenv)) {
+        if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, 8192 * 16 * sizeof(unsigned)));
+        if (grid > 8192) return -1;
+        HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 16 * sizeof(unsigned), stream()));
+        a.dbg = s_dbg;
+    }
+    fz::ffn fn = R == 1 ? fz::fused_fn<1>(sgn, conj) : R == 2 ? fz::fused_fn<2>(sgn, conj) : fz::fused_fn<4>(sgn, conj);
+    HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fz::LDS_BYTES));
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), fz::LDS_BYTES, stream(), a);
+    HCHK(hipGetLastError());
+    HCHK(hipMemcpyAsync(g_fz_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
+    if (a.dbg) { /* trace: per queue, tickets / A items / B items / spins summed over its workers */
+        static unsigned h[8192 * 16];
+        unsigned hc[16];
+        HCHK(hipStreamSynchronize(stream()));
+        HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 16 * sizeof(unsigned), hipMemcpyDeviceToHost));
+        HCHK(hipMemcpy(hc, ctr, sizeof hc, hipMemcpyDeviceToHost));
+        fprintf(stderr, "fz debug: R=%d ng=%u grid=%d heads", R, ng, grid);
+        for (int q = 0; q < 8; q++) fprintf(stderr, " %u", hc[q]);
+        fprintf(stderr, " err=%u done[0..3]=%u %u %u %u\n", hc[8], hc[12], ng > 1 ? hc[13] : 0, ng > 2 ? hc[14] : 0,
+                ng > 3 ? hc[15] : 0);
+        for (int q = 0; q < 8; q++) {
+            unsigned long long tk = 0, na = 0, nb = 0, sp = 0, ta = 0, tb = 0, tw = 0, pl = 0, pc = 0, ps = 0, pt = 0;
+            int workers = 0, idle = 0;
+            for (int b = q; b < grid; b += 8) {
+                tk += h[b * 16];
+                na += h[b * 16 + 2];
+                nb += h[b * 16 + 3];
+                sp += h[b * 16 + 4];
+                ta += h[b * 16 + 5];
+                tb += h[b * 16 + 6];
+                tw += h[b * 16 + 7];
+                pl += h[b * 16 + 8];
+                pc += h[b * 16 + 9];
+                ps += h[b * 16 + 10];
+                pt += h[b * 16 + 11];
+                workers++;
+                idle += h[b * 16] == 0;
+            }
+            fprintf(stderr,
+                    "  queue %d: workers %d (idle %d) tickets %llu A %llu B %llu spins %llu | us per A item %.2f, "
+                    "per B item %.2f, wait per B %.2f\n",
+                    q, workers, idle, tk, na, nb, sp, na ? ta / 100.0 / na : 0.0, nb ? tb / 100.0 / nb : 0.0,
+                    nb ? tw / 100.0 / nb : 0.0);
+            fprintf(stderr, "           A phases (us): load %.2f compute %.2f store-drain %.2f | ticket %.2f per item\n",
+                    na ? pl / 100.0 / na : 0.0, na ? pc / 100.0 / na : 0.0, na ? ps / 100.0 / na : 0.0,
+                    tk ? pt / 100.0 / tk : 0.0);
+        }
+    }
     return 0;
+}
+
+int hsd_cu_count(void)
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return n;
 }
 
 int hsd_select_stream(int idx)
@@ -494,7 +625,11 @@ const char *hsd_errstr(void) { return g_err; }
 
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
 {
-    if (p->variant == HS_KV_R8X3) return r8::launch(p, l, stream());
+    if (p->variant == HS_KV_R8X3) {
+        const int rc = pf::launch(p, l, stream());
+        if (rc <= 0) return rc;
+        return r8::launch(p, l, stream());
+    }
     if (p->variant == HS_KV_MR && l->load_op == HS_LOAD_PLAIN && l->store_op == HS_STORE_PLAIN)
         return mr::launch(p, l, stream());
     KArgs a;

@@ -559,6 +559,28 @@ static int run_pipelined(hs_entry *e, hs_devstate *ds, const void *I, long long 
     return rc;
 }
 
+/* 2^20 = [4,8,8,8 | 8,8,8] with plain loads/stores and contiguous output rows: both passes
+ * in one persistent launch (hsfft_fused.h), pass-B output in place on O */
+static int fused_rows(int batch)
+{
+    const int r = env_int("HSFFT_FZ_R", 2);
+    return (r == 1 || r == 2 || r == 4) && batch % r == 0 ? r : 1;
+}
+
+static int fused20_ok(const hs_entry *e, long long odist, int batch, int load_op, int store_op)
+{
+    if (!env_int("HSFFT_FUSED", 0) || e->M != (1 << 20) || e->npass != 2 || odist != e->M) return 0;
+    if (load_op != HS_LOAD_PLAIN || store_op != HS_STORE_PLAIN || batch < 1) return 0;
+    const hsd_pass *a = &e->pass[0], *b = &e->pass[1];
+    if (a->nst != 4 || !a->leaf || a->B != 1 || a->A != 512 || a->radix[0] != 4) return 0;
+    if (b->nst != 3 || b->B != 2048 || b->A != 1) return 0;
+    for (int s = 1; s < 4; s++)
+        if (a->radix[s] != 8) return 0;
+    for (int s = 0; s < 3; s++)
+        if (b->radix[s] != 8) return 0;
+    return 1;
+}
+
 /* One mixed-radix transform of length M per row, chained over the plan's passes.  Reads
  * I (never written), writes O.  Intermediate buffers come from the scratch pool; the last
  * pass (A == 1: it reads and writes the same element set per tile) may run in place on O
@@ -576,6 +598,15 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     }
     if (n == 1)
         return launch_pass(e, ds, 0, I, idist, O, odist, batch, sgn, conj, dir, load_op, laux, store_op, saux, nsig);
+    if (fused20_ok(e, odist, batch, load_op, store_op)) {
+        const int R = fused_rows(batch);
+        int grid = env_int("HSFFT_FZ_GRID", 0);
+        if (grid <= 0) grid = (hsd_cu_count() > 0 ? hsd_cu_count() : 256) * 2;
+        grid = (grid + 7) / 8 * 8;
+        int rc = hsd_fused20(I, idist, O, odist, ds->d_tw, batch, sgn, conj, R, env_int("HSFFT_FZ_LAG", 2), grid);
+        if (rc) hs_seterr("fused pass: %s", hsd_errstr());
+        return rc;
+    }
     const int last_inplace = store_op != HS_STORE_CHIRP && odist == M;
     /* passes 0..n-2 write scratch except that pass n-2 writes O when the last pass can run
      * in place; consecutive scratch writes alternate between two buffers */

@@ -105,6 +105,11 @@ int hsd_scale_real(void *x, long long n, int batch, long long dist, double divis
 int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
                   long long dlen, int batch);
 
+/* 2^20 = [4,8,8,8 | 8,8,8] as one persistent launch (hsfft_fused.h); rows of 2^20 complex */
+int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
+                int conj, int rows_per_group, int lag, int grid);
+int hsd_cu_count(void);
+
 /* timing on the library stream */
 int hsd_timer_start(void);
 int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *ms);

@@ -1,0 +1,388 @@
+/*
+ * hsfft_pass_pf.h -- software-pipelined register passes for the power-of-two hot path
+ * (BASELINE config 2: 2^20 = [4,8,8,8 | 8,8,8]; same shapes serve 2^18 / 2^21 / 2^22).
+ *
+ * Why a second family next to hsfft_pass_r8.h: a k_pass workgroup loads its tile, waits,
+ * computes and stores, so a CU only keeps HBM busy through the other resident workgroups
+ * (measured: ~4.8 TB/s per pass against a 6.0 TB/s copy of the same buffers).  Here every
+ * workgroup walks several tiles (first pass: TL column tiles of one row; later pass: T rows
+ * of one column tile) and issues the loads of tile i+1 before computing tile i, so 64 KiB
+ * per workgroup are always in flight.  That only works if nothing inside the loop waits on
+ * the vector-memory counter: the twiddles of every stage are the same for all tiles a
+ * workgroup walks (first pass: k = k_local; later pass: k = q + B*k_local with q fixed), so
+ * they are loaded once, before the loop, and kept in registers; the butterfly sign and the
+ * twiddle conjugation are template constants (conjugation applied once at load).
+ *
+ * Arithmetic is unchanged (hsfft_butterfly.h: the reference's operand order, no FMA), so
+ * results are bit-identical to k_pass and to the CPU reference.
+ */
+#pragma once
+
+namespace pf {
+
+using r8::Args;
+using r8::Shape;
+
+__device__ __forceinline__ unsigned xcd_remap(unsigned blk)
+{
+    const unsigned nwg = gridDim.x, q8 = nwg / 8, r8_ = nwg % 8, xcd = blk % 8;
+    return (xcd < r8_ ? xcd * (q8 + 1) : r8_ * (q8 + 1) + (xcd - r8_) * q8) + blk / 8;
+}
+
+/* twiddles of one radix-8 stage for a thread whose butterfly has k = k0 + B*kloc
+ * (ref :1310-1474: tw[L-1 + 7k + i-1], L = B*LLOC); CONJ negates the imaginary parts */
+template <bool CONJ>
+__device__ __forceinline__ void tw8(double2 (&w)[7], const double2 *tw, long long L, long long k)
+{
+    const double2 *p = tw + (L - 1 + 7 * k);
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        double2 v = p[i];
+        if (CONJ) v.y = -v.y;
+        w[i] = v;
+    }
+}
+
+/* one stage on this thread's 8 points: twiddles (radix-8 combine only) + 8/R butterflies */
+template <int R, int SGN>
+__device__ __forceinline__ void stage(double (&xr)[8], double (&xi)[8], const double2 (&w)[7], bool leaf)
+{
+    constexpr int NB = 8 / R;
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        if (!leaf) {
+#pragma unroll
+            for (int i = 1; i < R; i++) hsb::twmul(xr[c * R + i], xi[c * R + i], w[i - 1].x, w[i - 1].y);
+        }
+        hsb::bfly<R>(&xr[c * R], &xi[c * R], SGN, leaf);
+    }
+}
+
+/* global access as uniform base + 32-bit per-lane byte offset (saddr form: one VGPR of
+ * address per access instead of a 64-bit pair; rows are < 4 GiB) */
+__device__ __forceinline__ double2 ldg(const void *base, unsigned boff)
+{
+    return *(const double2 *)((const char *)base + boff);
+}
+__device__ __forceinline__ void stg(void *base, unsigned boff, double2 v) { *(double2 *)((char *)base + boff) = v; }
+
+/* ------------------------------------------------------------------ first pass
+ * [R0, 8^N8] leaf pass (B == 1): input [t][m] (t < P, m < A), output [m][u].  A workgroup
+ * owns G adjacent columns per tile and walks TL tiles of one row with stride `groups`, so the
+ * workgroups next to it (same XCD after xcd_remap) work on the neighbouring columns at the
+ * same time and each 128-B line is fetched into L2 once for 8/G of them. */
+template <int R0, int N8, int G>
+__device__ __forceinline__ void first_load(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned A,
+                                           unsigned m, int jt)
+{
+    constexpr int P = Shape<R0, N8>::P, TPG = Shape<R0, N8>::TPG, NB = 8 / R0, S0 = P / R0;
+    const unsigned lane = (jt * A + m) * 16u;
+#pragma unroll
+    for (int c = 0; c < NB; c++)
+#pragma unroll
+        for (int i = 0; i < R0; i++) {
+            const double2 v = ldg(row + (size_t)(c * TPG + i * S0) * A, lane);
+            xr[c * R0 + i] = v.x;
+            xi[c * R0 + i] = v.y;
+        }
+}
+
+/* twiddles of stage s of a first pass from the LDS copy of tw[0, P) */
+template <bool CONJ>
+__device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, int L, int kloc)
+{
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        double2 v = ltw[L - 1 + 7 * kloc + i];
+        if (CONJ) v.y = -v.y;
+        w[i] = v;
+    }
+}
+
+/* stages + exchanges + store of one first-pass tile held in xr/xi; ocol = output column */
+template <int R0, int N8, int G, int SGN, bool CONJ>
+__device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], double2 *lds, const double2 *ltw,
+                                           double2 *orow, unsigned m, int jt, int g)
+{
+    using S = Shape<R0, N8>;
+    constexpr int P = S::P, TPG = S::TPG;
+    double2 w[7];
+    stage<R0, SGN>(xr, xi, w, true);
+    if constexpr (N8 >= 1) {
+        r8::exchange<R0, 1, 8, TPG, P, G, true>(xr, xi, lds, jt, g);
+        tw8_lds<CONJ>(w, ltw, S::Lloc(1), jt & (S::Lloc(1) - 1));
+        stage<8, SGN>(xr, xi, w, false);
+    }
+    if constexpr (N8 >= 2) {
+        r8::exchange<8, S::Lloc(1), 8, TPG, P, G, true>(xr, xi, lds, jt, g);
+        tw8_lds<CONJ>(w, ltw, S::Lloc(2), jt & (S::Lloc(2) - 1));
+        stage<8, SGN>(xr, xi, w, false);
+    }
+    if constexpr (N8 >= 3) {
+        r8::exchange<8, S::Lloc(2), 8, TPG, P, G, true>(xr, xi, lds, jt, g);
+        tw8_lds<CONJ>(w, ltw, S::Lloc(3), jt & (S::Lloc(3) - 1));
+        stage<8, SGN>(xr, xi, w, false);
+    }
+    /* last stage: output u = jt + jj*LL of the column, written to [m][u] */
+    constexpr int LL = S::Lloc(S::NST - 1);
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
+}
+
+template <int R0, int N8, int G, int TL, int SGN, bool CONJ>
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
+{
+    using S = Shape<R0, N8>;
+    constexpr int P = S::P, TPG = S::TPG, NT = TPG * G;
+    static_assert(N8 >= 1, "leaf-only first passes use k_pass");
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    /* [0, P*G doubles): split exchange image; then tw[0, P): every twiddle a first pass of
+     * P points uses (stage L occupies [L-1, 8L-1), L < P) */
+    double2 *ltw = lds + P * G / 2;
+    const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
+    const unsigned groups = (unsigned)a.tiles_q; /* tile groups per row */
+    const unsigned b = blk / groups, tg = blk % groups;
+    const int tid0 = threadIdx.x;
+    const unsigned A = (unsigned)a.A;
+    const unsigned ntiles = A / G;
+
+    const double2 *row = a.in + (long long)b * a.idist;
+    double2 *orow = a.out + (long long)b * a.odist;
+    double pr[8], pi[8];
+    first_load<R0, N8, G>(pr, pi, row, A, tg * G + tid0 % G, tid0 / G);
+#pragma unroll
+    for (int i = tid0; i < P - 1; i += NT) ltw[i] = a.tw[i];
+    __syncthreads();
+    /* straight-line loop body (no branch around the prefetch: a conditional load makes the
+     * waitcnt pass drain vmcnt(0) at the loop header, stores included); the last tile runs
+     * after the loop without a prefetch */
+    const int nit = (int)((ntiles - 1 - tg) / groups + 1); /* tiles tg, tg+groups, ... < ntiles */
+    const unsigned mstep = groups * G;
+#pragma unroll 1
+    for (int it = 0; it < nit - 1; it++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const int g = tid % G, jt = tid / G;
+        const unsigned m = (tg + it * groups) * G + g;
+        double xr[8], xi[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            xr[i] = pr[i];
+            xi[i] = pi[i];
+        }
+        first_load<R0, N8, G>(pr, pi, row, A, m + mstep, jt);
+        first_body<R0, N8, G, SGN, CONJ>(xr, xi, lds, ltw, orow, m, jt, g);
+    }
+    {
+        const int g = tid0 % G, jt = tid0 / G;
+        const unsigned m = (tg + (nit - 1) * groups) * G + g;
+        first_body<R0, N8, G, SGN, CONJ>(pr, pi, lds, ltw, orow, m, jt, g);
+    }
+}
+
+/* ------------------------------------------------------------------ later pass [8,8,8]
+ * P = 512 at L = B (A == 1): input [t][q] (t < 512, q < B), output [u][q].  A workgroup
+ * owns 8 adjacent q-columns (128-B rows) and walks T rows of the batch; all three stages'
+ * twiddles (k = q + B*kloc) are row-independent and stay in registers. */
+/* stages + exchanges + store of one [8,8,8] tile-row; ocol = output row + q */
+template <int SGN>
+__device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], const double2 (&w2)[7], double2 *lds,
+                                          const double2 *ltw, double2 *orow, unsigned B, unsigned lane, int jt, int g)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    double2 w[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = ltw[7 * g + i];
+    stage<8, SGN>(xr, xi, w, false);
+    r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = ltw[56 * (1 + (jt & 7)) + 7 * g + i];
+    stage<8, SGN>(xr, xi, w, false);
+    r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    stage<8, SGN>(xr, xi, w2, false);
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) stg(orow + (size_t)jj * TPG * B, lane, make_double2(xr[jj], xi[jj]));
+}
+
+template <int T, int SGN, bool CONJ>
+__global__ __launch_bounds__(512, 4) void k_b512(Args a)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    /* [0, 4096): exchange image; then the stage-0 run (8 q x 7) and the 8 stage-1 runs
+     * (k_local = 0..7, 8 q x 7 each) of this tile's twiddles */
+    double2 *ltw = lds + P * G;
+    const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
+    const unsigned tiles = (unsigned)a.tiles;
+    const unsigned bg = blk / tiles, tile = blk % tiles;
+    const int tid0 = threadIdx.x;
+    const unsigned B = (unsigned)a.B;
+    const unsigned q0 = tile * G;
+    const unsigned b0 = bg * T, nb = (unsigned)a.batch;
+
+    double pr[8], pi[8];
+    {
+        const double2 *row = a.in + (long long)b0 * a.idist;
+        const unsigned lane = ((tid0 / G) * B + q0 + tid0 % G) * 16u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const double2 v = ldg(row + (size_t)i * TPG * B, lane);
+            pr[i] = v.x;
+            pi[i] = v.y;
+        }
+    }
+    /* stage-2 twiddles (k = q + B*k_local, k_local < 64): coalesced runs redistributed
+     * through this wave's slice of the image, kept in registers for all T rows */
+    double2 w2[7];
+    r8::load_tw_co<64>(w2, a, tid0 / G, q0);
+    if (tid0 < 504) {
+        const int r = tid0 / 56, e = tid0 % 56;
+        const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e
+                                     : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
+        double2 v = a.tw[src];
+        if (CONJ) v.y = -v.y;
+        ltw[tid0] = v;
+    }
+    r8::redistribute_tw(w2, lds);
+    if (CONJ) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) w2[i].y = -w2[i].y;
+    }
+    __syncthreads();
+
+    const int nit = (int)min((unsigned)T, nb - b0);
+#pragma unroll 1
+    for (int it = 0; it < nit - 1; it++) {
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const int g = tid % G, jt = tid / G;
+        const unsigned b = b0 + it, lane = (jt * B + q0 + g) * 16u;
+        double xr[8], xi[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            xr[i] = pr[i];
+            xi[i] = pi[i];
+        }
+        const double2 *row = a.in + (long long)(b + 1) * a.idist;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const double2 v = ldg(row + (size_t)i * TPG * B, lane);
+            pr[i] = v.x;
+            pi[i] = v.y;
+        }
+        b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
+    }
+    {
+        const int g = tid0 % G, jt = tid0 / G;
+        const unsigned b = b0 + nit - 1, lane = (jt * B + q0 + g) * 16u;
+        b512_body<SGN>(pr, pi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
+    }
+}
+
+/* ------------------------------------------------------------------ host side */
+typedef void (*kfn)(Args);
+
+inline int env(const char *name, int dflt)
+{
+    const char *s = getenv(name);
+    return s ? atoi(s) : dflt;
+}
+
+template <int R0, int N8, int G, int TL>
+inline kfn first_fn(int sgn, int conj)
+{
+    if (sgn == 1) return conj ? k_first<R0, N8, G, TL, 1, true> : k_first<R0, N8, G, TL, 1, false>;
+    return conj ? k_first<R0, N8, G, TL, -1, true> : k_first<R0, N8, G, TL, -1, false>;
+}
+
+template <int T>
+inline kfn b512_fn(int sgn, int conj)
+{
+    if (sgn == 1) return conj ? k_b512<T, 1, true> : k_b512<T, 1, false>;
+    return conj ? k_b512<T, -1, true> : k_b512<T, -1, false>;
+}
+
+/* the pipelined kernel for this pass, or nullptr (then hsfft_pass_r8.h's k_pass runs) */
+inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *threads, size_t *lds)
+{
+    const int mask = env("HSFFT_PF", 3); /* bit0: first pass, bit1: later [8,8,8] pass */
+    if (l->load_op != HS_LOAD_PLAIN || l->store_op != HS_STORE_PLAIN) return nullptr;
+    if (l->sgn != 1 && l->sgn != -1) return nullptr;
+    for (int s = 1; s < p->nst; s++)
+        if (p->radix[s] != 8) return nullptr;
+    if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 4) { /* 2^20's pass A: [4,8,8,8] */
+        const int g = env("HSFFT_PFG", 2), t = env("HSFFT_PFT", 4);
+        if (p->A % g) return nullptr;
+        *threads = 256 * g;
+        *lds = (size_t)2048 * g * sizeof(double) + 2048 * sizeof(double2);
+        *G = g;
+        if (g == 1) *TL = t >= 8 ? 8 : 4;
+        else if (g == 2) *TL = t >= 8 ? 8 : t >= 4 ? 4 : 2;
+        else if (g == 4) *TL = t >= 4 ? 4 : t >= 2 ? 2 : 1;
+        else return nullptr;
+        if (g == 1) return *TL == 8 ? first_fn<4, 3, 1, 8>(l->sgn, l->conj) : first_fn<4, 3, 1, 4>(l->sgn, l->conj);
+        if (g == 2)
+            return *TL == 8 ? first_fn<4, 3, 2, 8>(l->sgn, l->conj)
+                 : *TL == 4 ? first_fn<4, 3, 2, 4>(l->sgn, l->conj)
+                            : first_fn<4, 3, 2, 2>(l->sgn, l->conj);
+        return *TL == 4 ? first_fn<4, 3, 4, 4>(l->sgn, l->conj)
+             : *TL == 2 ? first_fn<4, 3, 4, 2>(l->sgn, l->conj)
+                        : first_fn<4, 3, 4, 1>(l->sgn, l->conj);
+    }
+    if ((mask & 2) && p->B > 1 && p->nst == 3 && p->radix[0] == 8 && p->A == 1 && p->B % 8 == 0) {
+        const int t = env("HSFFT_PFB", 8);
+        *TL = t >= 8 ? 8 : t >= 4 ? 4 : 2;
+        *G = 8;
+        *threads = 512;
+        *lds = (size_t)(512 * 8 + 504) * sizeof(double2);
+        return *TL == 8 ? b512_fn<8>(l->sgn, l->conj) : *TL == 4 ? b512_fn<4>(l->sgn, l->conj) : b512_fn<2>(l->sgn, l->conj);
+    }
+    return nullptr;
+}
+
+/* returns 1 if no pipelined kernel applies, 0 on launch, < 0 on error */
+inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
+{
+    int G = 0, TL = 0, threads = 0;
+    size_t lds = 0;
+    kfn fn = pick(p, l, &G, &TL, &threads, &lds);
+    if (!fn) return 1;
+    Args a;
+    memset(&a, 0, sizeof a);
+    a.in = (const double2 *)l->in;
+    a.out = (double2 *)l->out;
+    a.tw = (const double2 *)l->tw;
+    a.idist = l->idist;
+    a.odist = l->odist;
+    a.A = p->A;
+    a.B = p->B;
+    a.sgn = l->sgn;
+    a.dir = l->dir;
+    a.conj = l->conj;
+    a.xcd_groups = env("HSFFT_XCD", 1);
+    a.batch = l->batch;
+    long long grid;
+    if (p->B == 1) {
+        const long long ntiles = p->A / G, groups = (ntiles + TL - 1) / TL;
+        a.tiles_q = groups;
+        a.tiles = groups;
+        grid = groups * l->batch;
+    } else {
+        a.tiles = p->B / 8;
+        a.tiles_q = a.tiles;
+        grid = a.tiles * ((l->batch + TL - 1) / TL);
+    }
+    if (grid <= 0 || grid > 0x7fffffffLL) {
+        snprintf(g_err, sizeof g_err, "pf: bad grid %lld", grid);
+        return -1;
+    }
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return set_err(e, "hipFuncSetAttribute");
+    }
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(threads), lds, st, a);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace pf

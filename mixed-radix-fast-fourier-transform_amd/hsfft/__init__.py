@@ -200,6 +200,9 @@ class DeviceBuffer:
         check(lib().hsfft_memcpy_d2h(_ptr(out), VP(self.ptr + offset_bytes), out.nbytes), "d2h")
         return out
 
+    def fill_zero(self):
+        check(lib().hsfft_memset(self.ptr, 0, self.nbytes), "memset")
+
     def free(self):
         if self.ptr:
             lib().hsfft_free(self.ptr)
