@@ -168,6 +168,14 @@ def cpu_baseline(cfg, seconds_target=15.0):
                       f"one plan per thread, {secs:.2f} s wall"}
 
 
+def traffic_entry(cfg_name):
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(cfg_name) or {}
+    except (OSError, ValueError):
+        return {}
+
+
 def read_traffic(cfg_name, batch):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
     FETCH_SIZE x2 [gfx950 calibration] + WRITE_SIZE, per MI355X_MICROARCH.md §HBM), valid only
@@ -293,6 +301,9 @@ def main():
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
                            "kernel": f"pass {dom} of {npass}", "pass_ms": [round(p, 4) for p in pass_ms]}
+        ent = traffic_entry(args.config)
+        if dom == 0 and ent.get("kernel"):
+            out["roofline"]["kernel"] += f" ({ent['kernel'].replace('void ', '')})"
     else:
         ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -766,10 +766,12 @@ int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *
     hipEvent_t e0, e1;
     HCHK(hipEventCreate(&e0));
     HCHK(hipEventCreate(&e1));
-    hipLaunchKernelGGL(k_copy16, dim3(256 * 16), dim3(256), 0, stream(), (const double2 *)src, (double2 *)dst, n16);
+    /* the practical HBM ceiling: 4 x 16 B per lane in flight, 65536 x 256 threads (measured
+     * the fastest copy variant on 0.5-64 GiB buffers, tools/membench_sizes.py: 5.8-6.0 TB/s) */
+    hipLaunchKernelGGL((k_copyU<4, false>), dim3(65536), dim3(256), 0, stream(), (const v2d *)src, (v2d *)dst, n16);
     HCHK(hipEventRecord(e0, stream()));
     for (int i = 0; i < iters; i++)
-        hipLaunchKernelGGL(k_copy16, dim3(256 * 16), dim3(256), 0, stream(), (const double2 *)src, (double2 *)dst, n16);
+        hipLaunchKernelGGL((k_copyU<4, false>), dim3(65536), dim3(256), 0, stream(), (const v2d *)src, (v2d *)dst, n16);
     HCHK(hipEventRecord(e1, stream()));
     HCHK(hipEventSynchronize(e1));
     HCHK(hipEventElapsedTime(ms, e0, e1));

@@ -123,6 +123,33 @@ __device__ __forceinline__ void a_item(const FArgs &a, unsigned row, unsigned ti
         __builtin_amdgcn_raw_buffer_store_b128(as_u4(make_double2(xr[jj], xi[jj])), rs, lane, jj * 4096, 16);
 }
 
+/* pass A, two tiles ta, tb of `row` with the second tile's loads in flight during the first
+ * tile's stages (pf::k_first's body: split exchange in [0, 32 KiB), the first-pass twiddles
+ * tw[0, 2048) copied to [32, 64 KiB) per item), results stored write-through (sc1) */
+template <int SGN, bool CONJ>
+__device__ __forceinline__ void a_item2(const FArgs &a, unsigned row, unsigned ta, unsigned tb, double2 *lds, int tid)
+{
+    constexpr int G = 2;
+    double2 *ltw = lds + 2048;
+    const double2 *in = a.in + (long long)row * a.idist;
+    double2 *orow = a.out + (long long)row * a.odist;
+    const int g0 = tid & 1, jt0 = tid >> 1;
+    double xr[8], xi[8];
+    pf::first_load<4, 3, G>(xr, xi, in, 512u, ta * G + g0, jt0);
+#pragma unroll
+    for (int i = tid; i < 2047; i += 512) ltw[i] = a.tw[i];
+    __syncthreads();
+    double pr[8], pi[8];
+    pf::first_load<4, 3, G>(pr, pi, in, 512u, tb * G + g0, jt0);
+    {
+        int t = tid;
+        asm volatile("" : "+v"(t));
+        const int g = t & 1, jt = t >> 1;
+        pf::first_body<4, 3, G, SGN, CONJ, true>(xr, xi, lds, ltw, orow, ta * G + g, jt, g);
+    }
+    pf::first_body<4, 3, G, SGN, CONJ, true>(pr, pi, lds, ltw, orow, tb * G + g0, jt0, g0);
+}
+
 /* pass B, one tile (q-columns 8*qt .. 8*qt+7) over the R rows of group grp, reading the
  * intermediate with sc1 loads; output written in place with plain stores */
 template <int R, int SGN, bool CONJ>
@@ -195,7 +222,7 @@ __device__ __forceinline__ void b_item(const FArgs &a, unsigned grp, unsigned qt
 template <int R>
 __device__ __forceinline__ void decode(unsigned t, unsigned ng, unsigned lag, bool &isA, unsigned &grp, unsigned &i)
 {
-    constexpr unsigned nA = R * AT / NQ, nB = BT / NQ;
+    constexpr unsigned nA = R * AT / NQ / 2, nB = BT / NQ;
     const unsigned L = lag < ng ? lag : ng;
     if (t < L * nA) {
         isA = true;
@@ -225,22 +252,23 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
     unsigned *sticket = reinterpret_cast<unsigned *>(lds + 4096 + 504);
     const int tid = threadIdx.x;
     const unsigned x = blockIdx.x % NQ;
-    constexpr unsigned nA = R * AT / NQ, nB = BT / NQ;
+    constexpr unsigned nA = R * AT / NQ / 2, nB = BT / NQ, AQ = AT / NQ; /* A item = 2 tiles */
     const unsigned total = a.ngroups * (nA + nB);
     unsigned ntk = 0, na = 0, nb = 0, nspin = 0;
     /* last line of defence against a hang: a workgroup older than ~10 s (100 MHz real-time
      * counter) stops taking work and flags the call as failed */
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     constexpr unsigned long long T_LIMIT = 1ull << 30;
-    for (;;) {
-        const unsigned long long t_tk = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (tid == 0)
-            *sticket = __hip_atomic_fetch_add(&a.head[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const unsigned t = __builtin_amdgcn_readfirstlane(*sticket);
-        __syncthreads();
-        if (a.dbg && tid == 0) a.dbg[blockIdx.x * 16 + 11] += (unsigned)(__builtin_amdgcn_s_memrealtime() - t_tk);
-        if (t >= total) break;
+    if (tid == 0) *sticket = __hip_atomic_fetch_add(&a.head[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    unsigned t = __builtin_amdgcn_readfirstlane(*sticket);
+    __syncthreads();
+    while (t < total) {
+        /* the next ticket is fetched while this one is processed (its latency hidden); a
+         * fetched-but-unstarted A ticket cannot deadlock: every item waits only on items of
+         * an earlier queue phase, and this workgroup's current item precedes its next one */
+        unsigned tnext = 0;
+        if (tid == 0) tnext = __hip_atomic_fetch_add(&a.head[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__builtin_amdgcn_s_memrealtime() - t_start > T_LIMIT) {
             if (tid == 0) __hip_atomic_fetch_or(a.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
@@ -258,7 +286,8 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
         decode<R>(t, a.ngroups, a.lag, isA, grp, i);
         const unsigned long long t_item = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
         if (isA) {
-            a_item<SGN, CONJ>(a, grp * R + i / (AT / NQ), x * (AT / NQ) + i % (AT / NQ), lds, tid);
+            const unsigned row = grp * R + i / (AQ / 2), k = i % (AQ / 2);
+            a_item2<SGN, CONJ>(a, row, x * AQ + k, x * AQ + k + AQ / 2, lds, tid);
             const unsigned long long t_st = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* every storing wave: payload landed */
             if (a.dbg && tid == 0) a.dbg[blockIdx.x * 16 + 10] += (unsigned)(__builtin_amdgcn_s_memrealtime() - t_st);
@@ -270,7 +299,7 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
             }
         } else {
             if (tid == 0) {
-                const unsigned target = R * AT;
+                const unsigned target = R * AT / 2; /* A items (2 tiles each) of the group */
                 unsigned spins = 0;
                 while (__hip_atomic_load(&a.done[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                     __builtin_amdgcn_s_sleep(2);
@@ -292,6 +321,12 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
                 a.dbg[blockIdx.x * 16 + 6] += (unsigned)(__builtin_amdgcn_s_memrealtime() - t_b);
             }
         }
+        const unsigned long long t_tk = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (tid == 0) *sticket = tnext;
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(*sticket);
+        __syncthreads();
+        if (a.dbg && tid == 0) a.dbg[blockIdx.x * 16 + 11] += (unsigned)(__builtin_amdgcn_s_memrealtime() - t_tk);
     }
 }
 

@@ -100,7 +100,7 @@ __device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, int
 }
 
 /* stages + exchanges + store of one first-pass tile held in xr/xi; ocol = output column */
-template <int R0, int N8, int G, int SGN, bool CONJ>
+template <int R0, int N8, int G, int SGN, bool CONJ, bool SC1 = false>
 __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], double2 *lds, const double2 *ltw,
                                            double2 *orow, unsigned m, int jt, int g)
 {
@@ -126,7 +126,18 @@ __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], dou
     /* last stage: output u = jt + jj*LL of the column, written to [m][u] */
     constexpr int LL = S::Lloc(S::NST - 1);
 #pragma unroll
-    for (int jj = 0; jj < 8; jj++) stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
+    for (int jj = 0; jj < 8; jj++) {
+        if constexpr (SC1) { /* write-through for an in-launch consumer (hsfft_fused.h) */
+            typedef unsigned u4 __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(orow, 0, 0x7fffffff, 0x00020000);
+            const double2 v = make_double2(xr[jj], xi[jj]);
+            u4 u;
+            __builtin_memcpy(&u, &v, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(u, rs, (m * P + jt) * 16u, jj * LL * 16, 16);
+        } else {
+            stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
+        }
+    }
 }
 
 template <int R0, int N8, int G, int TL, int SGN, bool CONJ>
@@ -305,13 +316,15 @@ inline kfn b512_fn(int sgn, int conj)
 /* the pipelined kernel for this pass, or nullptr (then hsfft_pass_r8.h's k_pass runs) */
 inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *threads, size_t *lds)
 {
-    const int mask = env("HSFFT_PF", 3); /* bit0: first pass, bit1: later [8,8,8] pass */
+    /* bit0: first pass (default: 26.8 vs 28.0 ms per 4096 x 2^20), bit1: later [8,8,8] pass
+     * (opt-in: measured equal to k_pass_b512, 23.7 vs 23.5 ms) */
+    const int mask = env("HSFFT_PF", 1);
     if (l->load_op != HS_LOAD_PLAIN || l->store_op != HS_STORE_PLAIN) return nullptr;
     if (l->sgn != 1 && l->sgn != -1) return nullptr;
     for (int s = 1; s < p->nst; s++)
         if (p->radix[s] != 8) return nullptr;
     if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 4) { /* 2^20's pass A: [4,8,8,8] */
-        const int g = env("HSFFT_PFG", 2), t = env("HSFFT_PFT", 4);
+        const int g = env("HSFFT_PFG", 2), t = env("HSFFT_PFT", 8);
         if (p->A % g) return nullptr;
         *threads = 256 * g;
         *lds = (size_t)2048 * g * sizeof(double) + 2048 * sizeof(double2);
