@@ -127,13 +127,13 @@ __device__ __forceinline__ void a_item(const FArgs &a, unsigned row, unsigned ti
  * tile's stages (pf::k_first's body: split exchange in [0, 32 KiB), the first-pass twiddles
  * tw[0, 2048) copied to [32, 64 KiB) per item), results stored write-through (sc1) */
 template <int SGN, bool CONJ>
-__device__ __forceinline__ void a_item2(const FArgs &a, unsigned row, unsigned ta, unsigned tb, double2 *lds, int tid)
+__device__ __forceinline__ void a_item2(const FArgs &a, unsigned row, unsigned ta, unsigned tb, double2 *lds, unsigned tid)
 {
     constexpr int G = 2;
     double2 *ltw = lds + 2048;
     const double2 *in = a.in + (long long)row * a.idist;
     double2 *orow = a.out + (long long)row * a.odist;
-    const int g0 = tid & 1, jt0 = tid >> 1;
+    const unsigned g0 = tid & 1, jt0 = tid >> 1;
     double xr[8], xi[8];
     pf::first_load<4, 3, G>(xr, xi, in, 512u, ta * G + g0, jt0);
 #pragma unroll
@@ -142,9 +142,9 @@ __device__ __forceinline__ void a_item2(const FArgs &a, unsigned row, unsigned t
     double pr[8], pi[8];
     pf::first_load<4, 3, G>(pr, pi, in, 512u, tb * G + g0, jt0);
     {
-        int t = tid;
+        unsigned t = tid;
         asm volatile("" : "+v"(t));
-        const int g = t & 1, jt = t >> 1;
+        const unsigned g = t & 1, jt = t >> 1;
         pf::first_body<4, 3, G, SGN, CONJ, true>(xr, xi, lds, ltw, orow, ta * G + g, jt, g);
     }
     pf::first_body<4, 3, G, SGN, CONJ, true>(pr, pi, lds, ltw, orow, tb * G + g0, jt0, g0);
@@ -153,14 +153,14 @@ __device__ __forceinline__ void a_item2(const FArgs &a, unsigned row, unsigned t
 /* pass B, one tile (q-columns 8*qt .. 8*qt+7) over the R rows of group grp, reading the
  * intermediate with sc1 loads; output written in place with plain stores */
 template <int R, int SGN, bool CONJ>
-__device__ __forceinline__ void b_item(const FArgs &a, unsigned grp, unsigned qt, double2 *lds, int tid)
+__device__ __forceinline__ void b_item(const FArgs &a, unsigned grp, unsigned qt, double2 *lds, unsigned tid)
 {
     constexpr int P = 512, TPG = 64, G = 8;
     constexpr unsigned B = 2048;
     double2 *ltw = lds + P * G;
     const unsigned q0 = qt * G;
     const unsigned row0 = grp * R;
-    const int g0 = tid & 7, jt0 = tid >> 3;
+    const unsigned g0 = tid & 7, jt0 = tid >> 3;
     const unsigned lane0 = (jt0 * B + q0 + g0) * 16u;
     double pr[8], pi[8];
     {
@@ -195,9 +195,9 @@ __device__ __forceinline__ void b_item(const FArgs &a, unsigned grp, unsigned qt
     __syncthreads();
 #pragma unroll 1
     for (int it = 0; it < R - 1; it++) {
-        int t = tid;
+        unsigned t = tid;
         asm volatile("" : "+v"(t));
-        const int g = t & 7, jt = t >> 3;
+        const unsigned g = t & 7, jt = t >> 3;
         const unsigned lane = (jt * B + q0 + g) * 16u;
         double xr[8], xi[8];
 #pragma unroll
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     unsigned *sticket = reinterpret_cast<unsigned *>(lds + 4096 + 504);
-    const int tid = threadIdx.x;
+    const unsigned tid = threadIdx.x;
     const unsigned x = blockIdx.x % NQ;
     constexpr unsigned nA = R * AT / NQ / 2, nB = BT / NQ, AQ = AT / NQ; /* A item = 2 tiles */
     const unsigned total = a.ngroups * (nA + nB);

@@ -73,7 +73,7 @@ __device__ __forceinline__ void stg(void *base, unsigned boff, double2 v) { *(do
  * same time and each 128-B line is fetched into L2 once for 8/G of them. */
 template <int R0, int N8, int G>
 __device__ __forceinline__ void first_load(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned A,
-                                           unsigned m, int jt)
+                                           unsigned m, unsigned jt)
 {
     constexpr int P = Shape<R0, N8>::P, TPG = Shape<R0, N8>::TPG, NB = 8 / R0, S0 = P / R0;
     const unsigned lane = (jt * A + m) * 16u;
@@ -89,7 +89,7 @@ __device__ __forceinline__ void first_load(double (&xr)[8], double (&xi)[8], con
 
 /* twiddles of stage s of a first pass from the LDS copy of tw[0, P) */
 template <bool CONJ>
-__device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, int L, int kloc)
+__device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, unsigned L, unsigned kloc)
 {
 #pragma unroll
     for (int i = 0; i < 7; i++) {
@@ -102,7 +102,7 @@ __device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, int
 /* stages + exchanges + store of one first-pass tile held in xr/xi; ocol = output column */
 template <int R0, int N8, int G, int SGN, bool CONJ, bool SC1 = false>
 __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], double2 *lds, const double2 *ltw,
-                                           double2 *orow, unsigned m, int jt, int g)
+                                           double2 *orow, unsigned m, unsigned jt, unsigned g)
 {
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG;
@@ -153,7 +153,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
     const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
     const unsigned groups = (unsigned)a.tiles_q; /* tile groups per row */
     const unsigned b = blk / groups, tg = blk % groups;
-    const int tid0 = threadIdx.x;
+    const unsigned tid0 = threadIdx.x;
     const unsigned A = (unsigned)a.A;
     const unsigned ntiles = A / G;
 
@@ -171,9 +171,9 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
     const unsigned mstep = groups * G;
 #pragma unroll 1
     for (int it = 0; it < nit - 1; it++) {
-        int tid = tid0;
+        unsigned tid = tid0;
         asm volatile("" : "+v"(tid));
-        const int g = tid % G, jt = tid / G;
+        const unsigned g = tid % G, jt = tid / G;
         const unsigned m = (tg + it * groups) * G + g;
         double xr[8], xi[8];
 #pragma unroll
@@ -185,7 +185,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
         first_body<R0, N8, G, SGN, CONJ>(xr, xi, lds, ltw, orow, m, jt, g);
     }
     {
-        const int g = tid0 % G, jt = tid0 / G;
+        const unsigned g = tid0 % G, jt = tid0 / G;
         const unsigned m = (tg + (nit - 1) * groups) * G + g;
         first_body<R0, N8, G, SGN, CONJ>(pr, pi, lds, ltw, orow, m, jt, g);
     }
@@ -198,7 +198,8 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
 /* stages + exchanges + store of one [8,8,8] tile-row; ocol = output row + q */
 template <int SGN>
 __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], const double2 (&w2)[7], double2 *lds,
-                                          const double2 *ltw, double2 *orow, unsigned B, unsigned lane, int jt, int g)
+                                          const double2 *ltw, double2 *orow, unsigned B, unsigned lane, unsigned jt,
+                                          unsigned g)
 {
     constexpr int P = 512, TPG = 64, G = 8;
     double2 w[7];
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
     const unsigned tiles = (unsigned)a.tiles;
     const unsigned bg = blk / tiles, tile = blk % tiles;
-    const int tid0 = threadIdx.x;
+    const unsigned tid0 = threadIdx.x;
     const unsigned B = (unsigned)a.B;
     const unsigned q0 = tile * G;
     const unsigned b0 = bg * T, nb = (unsigned)a.batch;
@@ -264,9 +265,9 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     const int nit = (int)min((unsigned)T, nb - b0);
 #pragma unroll 1
     for (int it = 0; it < nit - 1; it++) {
-        int tid = tid0;
+        unsigned tid = tid0;
         asm volatile("" : "+v"(tid));
-        const int g = tid % G, jt = tid / G;
+        const unsigned g = tid % G, jt = tid / G;
         const unsigned b = b0 + it, lane = (jt * B + q0 + g) * 16u;
         double xr[8], xi[8];
 #pragma unroll
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
         b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
     }
     {
-        const int g = tid0 % G, jt = tid0 / G;
+        const unsigned g = tid0 % G, jt = tid0 / G;
         const unsigned b = b0 + nit - 1, lane = (jt * B + q0 + g) * 16u;
         b512_body<SGN>(pr, pi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
     }

@@ -127,7 +127,7 @@ __device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const
  * conflict, so the low bits are XOR-swizzled with the butterfly index (conflict-free
  * writes, and the reads of the next stage stay contiguous). */
 template <int R, int LLOC, int G>
-__device__ __forceinline__ int lds_slot(int p)
+__device__ __forceinline__ unsigned lds_slot(unsigned p)
 {
     if constexpr (LLOC == 1 && G < 8 && R > 1) return p ^ ((p / R) & (R - 1));
     return p;
@@ -145,28 +145,29 @@ __device__ __forceinline__ void pin(double (&x)[8])
 }
 
 template <int R, int LLOC, int R2, int TPG, int P, int G, bool SPLIT>
-__device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], double2 *lds, int jt, int g)
+__device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], double2 *lds, unsigned jt, unsigned g)
 {
+    /* unsigned index math throughout: signed / and % by powers of two cost sign fix-ups */
     constexpr int NB = 8 / R, NB2 = 8 / R2, L2 = LLOC * R, S2 = P / (L2 * R2);
     if constexpr (!SPLIT) {
 #pragma unroll
         for (int c = 0; c < NB; c++) {
-            const int b = c * TPG + jt;
-            const int kloc = b & (LLOC - 1), ml = b / LLOC;
+            const unsigned b = c * TPG + jt;
+            const unsigned kloc = b & (LLOC - 1), ml = b / LLOC;
 #pragma unroll
             for (int jj = 0; jj < R; jj++) {
-                const int p = lds_slot<R, LLOC, G>(ml * LLOC * R + kloc + jj * LLOC);
+                const unsigned p = lds_slot<R, LLOC, G>(ml * LLOC * R + kloc + jj * LLOC);
                 lds[p * G + g] = make_double2(xr[c * R + jj], xi[c * R + jj]);
             }
         }
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < NB2; c++) {
-            const int b = c * TPG + jt;
-            const int kloc = b & (L2 - 1), ml = b / L2;
+            const unsigned b = c * TPG + jt;
+            const unsigned kloc = b & (L2 - 1), ml = b / L2;
 #pragma unroll
             for (int i = 0; i < R2; i++) {
-                const int p = lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc);
+                const unsigned p = lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc);
                 const double2 v = lds[p * G + g];
                 xr[c * R2 + i] = v.x;
                 xi[c * R2 + i] = v.y;
@@ -182,16 +183,16 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
             double(&x)[8] = part ? xi : xr;
 #pragma unroll
             for (int c = 0; c < NB; c++) {
-                const int b = c * TPG + jt;
-                const int kloc = b & (LLOC - 1), ml = b / LLOC;
+                const unsigned b = c * TPG + jt;
+                const unsigned kloc = b & (LLOC - 1), ml = b / LLOC;
 #pragma unroll
                 for (int jj = 0; jj < R; jj++) ld[lds_slot<R, LLOC, G>(ml * LLOC * R + kloc + jj * LLOC) * G + g] = x[c * R + jj];
             }
             __syncthreads();
 #pragma unroll
             for (int c = 0; c < NB2; c++) {
-                const int b = c * TPG + jt;
-                const int kloc = b & (L2 - 1), ml = b / L2;
+                const unsigned b = c * TPG + jt;
+                const unsigned kloc = b & (L2 - 1), ml = b / L2;
 #pragma unroll
                 for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc) * G + g];
             }
