@@ -287,6 +287,40 @@ __global__ void k_r2c_post(const double2 *Z, const double2 *w2, double2 *X, int 
     }
 }
 
+/* same split, one thread per pair (k, h-k): Z is read once (k_r2c_post reads every element
+ * twice) and the four mirrored outputs X[k], X[N-k], X[h-k], X[h+k] are written together.
+ * Each output is computed by the reference's expression (real.c:112-122), so bit-identical. */
+__device__ __forceinline__ double2 r2c_bin(double2 a, double2 c, double2 w)
+{
+    const double t1 = a.y + c.y, t2 = c.x - a.x;
+    return make_double2((a.x + c.x + (t1 * w.x) + (t2 * w.y)) / 2.0, (a.y - c.y + (t2 * w.x) - (t1 * w.y)) / 2.0);
+}
+
+__global__ void k_r2c_post2(const double2 *Z, const double2 *w2, double2 *X, int h, long long zdist, long long xdist)
+{
+    const int b = blockIdx.y;
+    const double2 *z = Z + b * zdist;
+    double2 *x = X + b * xdist;
+    const int N = 2 * h, half = h / 2;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= half; k += gridDim.x * blockDim.x) {
+        if (k == 0) {
+            const double2 z0 = z[0];
+            x[0] = make_double2(z0.x + z0.y, 0.0);
+            x[h] = make_double2(z0.x - z0.y, 0.0);
+            continue;
+        }
+        const double2 a = z[k], c = z[h - k];
+        const double2 lo = r2c_bin(a, c, w2[k]);
+        x[k] = lo;
+        x[N - k] = make_double2(lo.x, -lo.y);
+        if (k != h - k) {
+            const double2 hi = r2c_bin(c, a, w2[h - k]);
+            x[h - k] = hi;
+            x[h + k] = make_double2(hi.x, -hi.y);
+        }
+    }
+}
+
 /* ref real.c:169-179 */
 __global__ void k_c2r_pre(const double2 *X, const double2 *w2, double2 *Zi, int h, long long xdist, long long zdist)
 {
@@ -719,8 +753,13 @@ int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset)
 int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
 {
     if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_r2c_post, dim3(grid_for(h + 1, 256), batch), dim3(256), 0, stream(), (const double2 *)Z,
-                       (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
+    const char *e = getenv("HSFFT_R2C_POST");
+    if (e && atoi(e) == 1)
+        hipLaunchKernelGGL(k_r2c_post, dim3(grid_for(h + 1, 256), batch), dim3(256), 0, stream(), (const double2 *)Z,
+                           (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
+    else
+        hipLaunchKernelGGL(k_r2c_post2, dim3(grid_for(h / 2 + 1, 256), batch), dim3(256), 0, stream(),
+                           (const double2 *)Z, (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
     HCHK(hipGetLastError());
     return 0;
 }
