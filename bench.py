@@ -201,6 +201,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
     ap.add_argument("--dry-n", type=int, default=1024)
+    ap.add_argument("--host-rows", type=int, default=0,
+                    help="also time hsfft_exec_batched_host on this many HOST-resident rows (PCIe-inclusive "
+                         "rate, reported as host_pipeline; never the headline value)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -313,6 +316,19 @@ def main():
     nbytes = min(din.nbytes, dout.nbytes) // 16 * 16
     cms = hsfft.bench_copy(din, dout, nbytes, 5)
     out["stream_copy_gbs"] = round(2 * nbytes * 5 / (cms / 1e3) / 1e9, 1)
+    if args.host_rows and kind == "c2c":
+        import numpy as np
+        hb = min(args.host_rows, batch)
+        hx = din.to_array(np.complex128, hb * n).reshape(hb, n)
+        hy = np.empty_like(hx)
+        hsfft.exec_batched_host(plan, hx, hy)  # warm-up (plan state, staging slots)
+        t0 = time.perf_counter()
+        hsfft.exec_batched_host(plan, hx, hy)
+        hs = time.perf_counter() - t0
+        out["host_pipeline"] = {"rows": hb, "gsamples_s": round(hb * n / hs / 1e9, 3),
+                                "pcie_gbs": round(2 * hx.nbytes / hs / 1e9, 1),
+                                "note": "host (pageable numpy) rows in and out, upload/transform/download overlapped; "
+                                        "PCIe-inclusive, not the headline value"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:

@@ -59,6 +59,10 @@ int hsfft_digit_reverse_map(fft_object obj, int *map);
 /* --- batched, device-resident execution ------------------------------------------------ */
 /* c2c: d_in, d_out hold batch*N complex; d_in is not modified; d_in != d_out. */
 int hsfft_exec_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch);
+/* c2c on HOST-resident rows (the drop-in case of a caller that never touches HBM): rows are
+ * streamed through HBM in chunks with upload / transform / download overlapped on three
+ * streams; caller buffers are page-locked for the call where possible.  Synchronous. */
+int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_out, int batch);
 /* r2c in the reference layout: batch rows of N reals -> batch rows of N complex (mirrored) */
 int hsfft_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out, int batch);
 /* c2r: batch rows of N complex (first N/2+1 read) -> batch rows of N reals */

@@ -40,9 +40,9 @@ int set_err(hipError_t e, const char *what)
         if (e_ != hipSuccess) return set_err(e_, #call);                \
     } while (0)
 
-hipStream_t g_stream2[HS_MAX_DEV];
-bool g_stream2_init[HS_MAX_DEV];
-thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline stream */
+hipStream_t g_stream2[HS_MAX_DEV], g_stream3[HS_MAX_DEV];
+bool g_stream2_init[HS_MAX_DEV], g_stream3_init[HS_MAX_DEV];
+thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream */
 
 hipStream_t primary()
 {
@@ -62,6 +62,13 @@ hipStream_t stream()
     if (t_sidx == 0) return primary();
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) dev = 0;
+    if (t_sidx == 2) {
+        if (!g_stream3_init[dev]) {
+            if (hipStreamCreateWithFlags(&g_stream3[dev], hipStreamNonBlocking) != hipSuccess) g_stream3[dev] = 0;
+            g_stream3_init[dev] = true;
+        }
+        return g_stream3[dev];
+    }
     if (!g_stream2_init[dev]) {
         if (hipStreamCreateWithFlags(&g_stream2[dev], hipStreamNonBlocking) != hipSuccess) g_stream2[dev] = 0;
         g_stream2_init[dev] = true;
@@ -615,7 +622,39 @@ int hsd_cu_count(void)
 
 int hsd_select_stream(int idx)
 {
-    t_sidx = idx ? 1 : 0;
+    t_sidx = idx < 0 || idx > 2 ? 0 : idx;
+    return 0;
+}
+
+int hsd_h2d_async(void *d, const void *h, size_t bytes)
+{
+    HCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream()));
+    return 0;
+}
+
+int hsd_d2h_async(void *h, const void *d, size_t bytes)
+{
+    HCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream()));
+    return 0;
+}
+
+int hsd_stream_sync(void)
+{
+    HCHK(hipStreamSynchronize(stream()));
+    return 0;
+}
+
+/* page-lock caller memory for asynchronous copies; 1 if this call registered it */
+int hsd_host_register(void *p, size_t bytes)
+{
+    if (hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess) return 1;
+    (void)hipGetLastError(); /* already pinned (hipHostMalloc'd / registered) or not pinnable */
+    return 0;
+}
+
+int hsd_host_unregister(void *p)
+{
+    HCHK(hipHostUnregister(p));
     return 0;
 }
 

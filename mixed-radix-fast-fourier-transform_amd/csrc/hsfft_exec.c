@@ -838,6 +838,68 @@ int hsfft_exec_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
     return hs_c2c_rows(e, d_in, obj->N, d_out, obj->N, batch);
 }
 
+/* Host-resident batch: rows are streamed through two HBM staging
+ * slots in chunks, H2D on stream 1, the transform on the library stream, D2H on stream 2,
+ * ordered by events so that chunk k+1's upload and chunk k-1's download overlap chunk k's
+ * transform (PCIe-bound).  Caller buffers are page-locked for the call when possible. */
+static size_t host_chunk_bytes(void)
+{
+    const char *s = getenv("HSFFT_HOST_CHUNK_MB");
+    size_t v = (size_t)(s ? atof(s) : 256.0) * (1u << 20);
+    return v < (1u << 20) ? (1u << 20) : v;
+}
+
+int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_out, int batch)
+{
+    g_errbuf[0] = 0;
+    if (!obj || !h_in || !h_out || batch < 0 || h_in == h_out) {
+        hs_seterr("hsfft_exec_batched_host: invalid arguments");
+        return HSFFT_ERR_ARG;
+    }
+    if (batch == 0) return 0;
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    hs_entry *e = hs_entry_get(obj);
+    if (!e) return HSFFT_ERR_ARG;
+    const long long N = obj->N;
+    const size_t row = sizeof(fft_data) * (size_t)N, total = row * (size_t)batch;
+    long long chunk = (long long)(host_chunk_bytes() / row);
+    if (chunk < 1) chunk = 1;
+    if (chunk > batch) chunk = batch;
+    fft_data *din = hs_scratch(7, 2 * row * (size_t)chunk), *dout = hs_scratch(9, 2 * row * (size_t)chunk);
+    if (!din || !dout) return HSFFT_ERR_NOMEM;
+    const int reg_in = hsd_host_register((void *)h_in, total), reg_out = hsd_host_register(h_out, total);
+    enum { EV_H = 40, EV_X = 42, EV_D = 44 };
+    int k = 0;
+    for (long long c0 = 0; c0 < batch && !rc; c0 += chunk, k++) {
+        const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk), sl = k & 1;
+        fft_data *di = din + (size_t)sl * chunk * N, *dq = dout + (size_t)sl * chunk * N;
+        hsd_select_stream(1);
+        if (k >= 2) rc = hsd_event_wait(EV_X + sl); /* slot's previous transform has read di */
+        if (!rc) rc = hsd_h2d_async(di, h_in + c0 * N, row * (size_t)cb);
+        if (!rc) rc = hsd_event_record(EV_H + sl);
+        hsd_select_stream(0);
+        if (!rc) rc = hsd_event_wait(EV_H + sl);
+        if (!rc && k >= 2) rc = hsd_event_wait(EV_D + sl); /* slot's previous output is home */
+        if (!rc) rc = hs_c2c_rows(e, di, N, dq, N, cb);
+        if (!rc) rc = hsd_event_record(EV_X + sl);
+        hsd_select_stream(2);
+        if (!rc) rc = hsd_event_wait(EV_X + sl);
+        if (!rc) rc = hsd_d2h_async(h_out + c0 * N, dq, row * (size_t)cb);
+        if (!rc) rc = hsd_event_record(EV_D + sl);
+    }
+    for (int st = 2; st >= 0; st--) {
+        hsd_select_stream(st);
+        if (hsd_stream_sync() && !rc) rc = HSFFT_ERR_DEVICE;
+    }
+    hsd_select_stream(0);
+    if (!rc && hsd_sync()) rc = HSFFT_ERR_DEVICE;
+    if (reg_in) hsd_host_unregister((void *)h_in);
+    if (reg_out) hsd_host_unregister(h_out);
+    if (rc && !g_errbuf[0]) hs_seterr("hsfft_exec_batched_host: %s", hsd_errstr());
+    return rc < 0 ? rc : (rc ? HSFFT_ERR_DEVICE : 0);
+}
+
 int hsfft_fill_complex(fft_data *d_x, int64_t count, uint64_t seed, uint64_t offset)
 {
     int rc = hs_require_gpu();

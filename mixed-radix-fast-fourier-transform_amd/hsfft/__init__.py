@@ -53,6 +53,7 @@ SIGNATURES = {
     "hsfft_plan_num_passes": (CI, [VP]),
     "hsfft_digit_reverse_map": (CI, [VP, VP]),
     "hsfft_exec_batched": (CI, [VP, VP, VP, CI]),
+    "hsfft_exec_batched_host": (CI, [VP, VP, VP, CI]),
     "hsfft_r2c_batched": (CI, [VP, VP, VP, CI]),
     "hsfft_c2r_batched": (CI, [VP, VP, VP, CI]),
     "hsfft_convolve_batched": (CI, [ctypes.c_char_p, ctypes.c_char_p, VP, CI, VP, CI, VP, CI]),
@@ -217,6 +218,15 @@ class DeviceBuffer:
 
 def exec_batched(plan, d_in, d_out, batch):
     return check(lib().hsfft_exec_batched(plan.ptr, VP(d_in.ptr), VP(d_out.ptr), batch), "exec_batched")
+
+
+def exec_batched_host(plan, x, out=None):
+    """c2c of host rows x (batch, N) complex128 through hsfft_exec_batched_host"""
+    x = np.ascontiguousarray(x, dtype=np.complex128)
+    out = np.empty_like(x) if out is None else out
+    batch = x.shape[0] if x.ndim == 2 else 1
+    check(lib().hsfft_exec_batched_host(plan.ptr, _ptr(x), _ptr(out), batch), "exec_batched_host")
+    return out
 
 
 def r2c_batched(rplan, d_in, d_out, batch):

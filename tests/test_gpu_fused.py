@@ -106,3 +106,15 @@ def test_fused_large_batch_vs_two_launch(monkeypatch):
         assert T.bits_equal(a[row * N:(row + 1) * N], T.oracle_c2c(x, 1)), row
     for d in (din, d1, d2):
         d.free()
+
+
+@pytest.mark.parametrize("n,batch,chunk_mb", [(1 << 20, 7, "32"), (4096, 33, "1"), (12600, 5, "1"), (99991, 3, "2")])
+def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
+    """hsfft_exec_batched_host (host rows streamed through HBM in chunks, upload / transform /
+    download on three streams): bit-exact vs the oracle, odd chunk counts included."""
+    monkeypatch.setenv("HSFFT_HOST_CHUNK_MB", chunk_mb)
+    x = T.complex_input(n, 0xAB ^ n, batch=batch).reshape(batch, n)
+    p = hsfft.Plan(n, 1)
+    y = hsfft.exec_batched_host(p, x)
+    assert T.bits_equal(y, T.oracle_c2c(x, 1)), n
+    p.close()
