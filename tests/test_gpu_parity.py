@@ -328,3 +328,61 @@ def test_r2c_fused_split_opt_in(n, monkeypatch):
     hsfft.r2c_batched(rp, din, dout, 2)
     y = dout.to_array(np.complex128).reshape(2, n)
     assert T.bits_equal(y, T.oracle_r2c(x, 1))
+
+
+def _full_size_c2c(n, batch, seed, rows, sgn=1, tol=1e-13, roundtrip=True):
+    """a BASELINE config at its full per-GPU batch: sampled rows bit-exact vs the oracle and
+    a forward/inverse round trip of the first rows (size-independent properties)."""
+    p, pi = hsfft.Plan(n, sgn), hsfft.Plan(n, -sgn)
+    din = hsfft.DeviceBuffer(batch * n * 16)
+    dout = hsfft.DeviceBuffer(batch * n * 16)
+    hsfft.fill_complex(din, batch * n, seed)
+    hsfft.exec_batched(p, din, dout, batch)
+    hsfft.synchronize()
+    for row in rows:
+        y = dout.to_array(np.complex128, n, row * n * 16)
+        x = T.complex_input(n, seed, batch=1, row0=row)
+        assert T.bits_equal(y, oracle_rows(x, sgn)), row
+    if roundtrip:
+        hsfft.exec_batched(pi, dout, din, 4)
+        hsfft.synchronize()
+        z = din.to_array(np.complex128, 4 * n).reshape(4, n) / n
+        x = T.complex_input(n, seed, batch=4).reshape(4, n)
+        assert np.abs(z - x).max() < tol
+    din.free()
+    dout.free()
+
+
+def test_full_size_config3_12600_x_65536():
+    """config 3 at full size (65536 rows, 13 GB each way), bit-exact in the reference twiddle
+    mode (whose D2 tables are not an exact inverse pair, so the round trip is checked in
+    exact mode, limited by the reference's 11-digit radix-3/5/7 constants)"""
+    _full_size_c2c(12600, 65536, T.SEEDS[3], (0, 40000, 65535), roundtrip=False)
+    hsfft.set_twiddle_mode("exact")
+    try:
+        _full_size_c2c(12600, 2048, T.SEEDS[3], (0, 2047), tol=1e-9)
+    finally:
+        hsfft.set_twiddle_mode("reference")
+
+
+def test_full_size_config4_bluestein_99991_x_8192():
+    _full_size_c2c(99991, 8192, T.SEEDS[4], (0, 5000, 8191), tol=1e-10)
+
+
+def test_full_size_config5_r2c_2pow22_rows():
+    """config 5's row length (2^22 reals) at 512 rows per call (one GPU's 4096-row shard runs
+    in 8 such calls in bench.py): sampled rows bit-exact vs the oracle, Hermitian mirror"""
+    n, batch = 1 << 22, 512
+    rp = hsfft.RealPlan(n, 1)
+    din = hsfft.DeviceBuffer(batch * n * 8)
+    dout = hsfft.DeviceBuffer(batch * n * 16)
+    hsfft.fill_real(din, batch * n, T.SEEDS[5])
+    hsfft.r2c_batched(rp, din, dout, batch)
+    hsfft.synchronize()
+    for row in (0, 311, batch - 1):
+        y = dout.to_array(np.complex128, n, row * n * 16)
+        x = T.real_input(n, T.SEEDS[5], batch=1, row0=row)
+        assert T.bits_equal(y, T.oracle_r2c(x.reshape(1, n), 1)[0]), row
+        assert np.array_equal(y[1:n // 2], np.conj(y[n - 1:n // 2:-1]))
+    din.free()
+    dout.free()
