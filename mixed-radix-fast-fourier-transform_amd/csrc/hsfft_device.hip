@@ -419,6 +419,7 @@ int grid_for(long long n, int threads)
 #include "hsfft_pass_mr.h"
 #include "hsfft_pass_pf.h"
 #include "hsfft_fused.h"
+#include "hsfft_blue_pf.h"
 
 extern "C" {
 
@@ -758,7 +759,23 @@ int r8_has_variant(int r0, int n8, int G, int Wq, int first) { return r8::find(r
 int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
                  int conj, int dir, int sgn2, int conj2)
 {
+    if (conj == 0 && dir == sgn && sgn2 == -sgn && conj2 == 1) {
+        const int rc = bpf::launch(0, in, dist, out, dist, tw, hk, 0, batch, sgn, stream());
+        if (rc <= 0) return rc;
+    }
     return r8::launch_blue_mid(in, out, dist, tw, hk, batch, sgn, conj, dir, sgn2, conj2, stream());
+}
+
+int hsd_blue_last(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                  long long nsig, int batch, int dir)
+{
+    return bpf::launch(1, in, idist, out, odist, tw, chirp, nsig, batch, dir, stream());
+}
+
+int hsd_blue_first(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                   long long nsig, int batch, int dir)
+{
+    return bpf::launch(2, in, idist, out, odist, tw, chirp, nsig, batch, dir, stream());
 }
 
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,

@@ -693,15 +693,22 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
     if (fuse && !mid2) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch && fuse; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
-        int rc = launch_pass(e, ds, 0, (const fft_data *)in + c0 * idist, idist, mid, M, cb, e->sgn, 0, e->sgn,
+        int rc = hsd_blue_first((const fft_data *)in + c0 * idist, idist, mid, M, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
+        if (rc < 0) hs_seterr("bluestein first pass: %s", hsd_errstr());
+        if (rc == 1)
+            rc = launch_pass(e, ds, 0, (const fft_data *)in + c0 * idist, idist, mid, M, cb, e->sgn, 0, e->sgn,
                              HS_LOAD_CHIRP, ds->d_chirp, HS_STORE_PLAIN, NULL, N);
         if (!rc && hsd_blue_mid(mid, mid2, M, ds->d_tw, ds->d_hk, cb, e->sgn, 0, e->sgn, -1 * e->sgn, 1)) {
             hs_seterr("bluestein middle: %s", hsd_errstr());
             rc = HSFFT_ERR_DEVICE;
         }
-        if (!rc)
-            rc = launch_pass(e, ds, 1, mid2, M, (fft_data *)out + c0 * odist, odist, cb, -1 * e->sgn, 1, e->sgn,
-                             HS_LOAD_PLAIN, NULL, HS_STORE_CHIRP, ds->d_chirp, N);
+        if (!rc) {
+            rc = hsd_blue_last(mid2, M, (fft_data *)out + c0 * odist, odist, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
+            if (rc < 0) hs_seterr("bluestein last pass: %s", hsd_errstr());
+            if (rc == 1)
+                rc = launch_pass(e, ds, 1, mid2, M, (fft_data *)out + c0 * odist, odist, cb, -1 * e->sgn, 1, e->sgn,
+                                 HS_LOAD_PLAIN, NULL, HS_STORE_CHIRP, ds->d_chirp, N);
+        }
         if (rc) return rc;
     }
     for (long long c0 = 0; c0 < batch && !fuse; c0 += chunk) {

@@ -98,6 +98,13 @@ int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
 int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
                  int conj, int dir, int sgn2, int conj2); /* hsfft_pass_mr.h has a kernel for this pass */
+/* Bluestein M = 2^18: inverse last pass stored through the chirp (rows of M -> rows of N);
+ * 1 if the row-looped kernel is disabled (caller runs the generic pass) */
+int hsd_blue_last(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                  long long nsig, int batch, int dir);
+/* Bluestein M = 2^18: forward first pass on the chirped input (rows of N -> rows of M) */
+int hsd_blue_first(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                   long long nsig, int batch, int dir);
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset);
 int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset);
 /* r2c split (real.c:108-132): Z rows of h complex -> X rows of 2h complex */

@@ -118,3 +118,25 @@ def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
     y = hsfft.exec_batched_host(p, x)
     assert T.bits_equal(y, T.oracle_c2c(x, 1)), n
     p.close()
+
+
+@pytest.mark.parametrize("mask,t", [("0", "4"), ("3", "1"), ("3", "2"), ("3", "4"), ("3", "8"), ("1", "4"), ("2", "4")])
+@pytest.mark.parametrize("n", [99991, 65537, 131071])
+def test_bluestein_row_looped_kernels(n, mask, t, monkeypatch):
+    """Bluestein with M = 2^18 (config 4's size; 65537 = 2^16+1 is the plan/exec M mismatch
+    case D5, computed with its own exec-length table): the row-looped middle / last kernels
+    (csrc/hsfft_blue_pf.h) for every tile-row count, odd batch, both signs, bit-exact."""
+    monkeypatch.setenv("HSFFT_BLUE_PF", mask)
+    monkeypatch.setenv("HSFFT_BLUE_T", t)
+    x = T.complex_input(n, 0xB1 ^ n, batch=5).reshape(5, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, 5)
+        hsfft.synchronize()
+        y = dout.to_array(np.complex128).reshape(5, n)
+        assert T.bits_equal(y, _oracle(x, sgn, ("blue", n))), (n, sgn, mask, t)
+        din.free()
+        dout.free()
+        p.close()
