@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch (development only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--r2c-compact", action="store_true",
+                    help="c5 only: hsfft_r2c_batched_compact (N/2+1 bins per row) instead of the reference layout")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
     ap.add_argument("--dry-n", type=int, default=1024)
     ap.add_argument("--host-rows", type=int, default=0,
@@ -220,6 +222,8 @@ def main():
 
     cfg = CONFIGS[args.config]
     kind, n, batch, seed, desc = cfg
+    if args.r2c_compact and kind == "r2c":
+        desc += " [compact N/2+1 output, hsfft_r2c_batched_compact]"
     if args.batch:
         batch = args.batch
     samples = n * batch
@@ -239,15 +243,18 @@ def main():
         # so the step writes it chunk by chunk into one output buffer a consumer would drain
         chunk = min(batch, max(1, (64 << 30) // (n * 16)))
         din = hsfft.DeviceBuffer(samples * 8)
-        dout = hsfft.DeviceBuffer(chunk * n * 16)
+        orow = (n // 2 + 1) if args.r2c_compact else n
+        dout = hsfft.DeviceBuffer(chunk * orow * 16)
         hsfft.fill_real(din, samples, seed, row_range(rank, batch)[0] * n)
+        fn = hsfft.lib().hsfft_r2c_batched_compact if args.r2c_compact else hsfft.lib().hsfft_r2c_batched
 
         def run():
             for c0 in range(0, batch, chunk):
                 cb = min(chunk, batch - c0)
-                hsfft.check(hsfft.lib().hsfft_r2c_batched(plan.ptr, ctypes.c_void_p(din.ptr + c0 * n * 8),
-                                                          ctypes.c_void_p(dout.ptr), cb), "r2c_batched")
-        bytes_per_sample = 24  # read 8 B + write 16 B of the mirrored output
+                hsfft.check(fn(plan.ptr, ctypes.c_void_p(din.ptr + c0 * n * 8), ctypes.c_void_p(dout.ptr), cb),
+                            "r2c_batched")
+        # read 8 B + write 16 B of the mirrored output (compact: 8 B of the N/2+1 bins)
+        bytes_per_sample = 16 if args.r2c_compact else 24
         dtype = "f64"
     hsfft.synchronize()
 
@@ -272,6 +279,8 @@ def main():
         ev_ms, pms = hsfft.time_batched(plan, din, dout, batch, max(1, args.steps))
         npass = plan.num_passes()
         pass_ms = [p for p in pms[:npass] if p > 0]
+    elif args.r2c_compact:
+        ev_ms = wall * 1e3
     else:
         ev_ms = hsfft.time_r2c_batched(plan, din, dout, chunk, max(1, args.steps)) * (batch / chunk)
     ev_step_ms = comm.max(ev_ms / max(1, args.steps))

@@ -65,6 +65,9 @@ int hsfft_exec_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
 int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_out, int batch);
 /* r2c in the reference layout: batch rows of N reals -> batch rows of N complex (mirrored) */
 int hsfft_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out, int batch);
+/* r2c, compact layout: batch rows of N reals -> batch rows of N/2+1 complex (bins 0..N/2,
+ * identical to the first N/2+1 bins of hsfft_r2c_batched; one third less HBM written) */
+int hsfft_r2c_batched_compact(fft_real_object obj, const fft_type *d_in, fft_data *d_out, int batch);
 /* c2r: batch rows of N complex (first N/2+1 read) -> batch rows of N reals */
 int hsfft_c2r_batched(fft_real_object obj, const fft_data *d_in, fft_type *d_out, int batch);
 /* batched linear/circular convolution of equal-length real rows (reference semantics of

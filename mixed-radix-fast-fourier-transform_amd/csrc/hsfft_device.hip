@@ -303,6 +303,7 @@ __device__ __forceinline__ double2 r2c_bin(double2 a, double2 c, double2 w)
     return make_double2((a.x + c.x + (t1 * w.x) + (t2 * w.y)) / 2.0, (a.y - c.y + (t2 * w.x) - (t1 * w.y)) / 2.0);
 }
 
+template <bool COMPACT>
 __global__ void k_r2c_post2(const double2 *Z, const double2 *w2, double2 *X, int h, long long zdist, long long xdist)
 {
     const int b = blockIdx.y;
@@ -319,11 +320,11 @@ __global__ void k_r2c_post2(const double2 *Z, const double2 *w2, double2 *X, int
         const double2 a = z[k], c = z[h - k];
         const double2 lo = r2c_bin(a, c, w2[k]);
         x[k] = lo;
-        x[N - k] = make_double2(lo.x, -lo.y);
+        if (!COMPACT) x[N - k] = make_double2(lo.x, -lo.y);
         if (k != h - k) {
             const double2 hi = r2c_bin(c, a, w2[h - k]);
             x[h - k] = hi;
-            x[h + k] = make_double2(hi.x, -hi.y);
+            if (!COMPACT) x[h + k] = make_double2(hi.x, -hi.y);
         }
     }
 }
@@ -814,8 +815,18 @@ int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long
         hipLaunchKernelGGL(k_r2c_post, dim3(grid_for(h + 1, 256), batch), dim3(256), 0, stream(), (const double2 *)Z,
                            (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
     else
-        hipLaunchKernelGGL(k_r2c_post2, dim3(grid_for(h / 2 + 1, 256), batch), dim3(256), 0, stream(),
+        hipLaunchKernelGGL(k_r2c_post2<false>, dim3(grid_for(h / 2 + 1, 256), batch), dim3(256), 0, stream(),
                            (const double2 *)Z, (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+/* bins 0..h only (rows of h+1 complex): the non-redundant half of real.c's mirrored output */
+int hsd_r2c_post_compact(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_r2c_post2<true>, dim3(grid_for(h / 2 + 1, 256), batch), dim3(256), 0, stream(),
+                       (const double2 *)Z, (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
     HCHK(hipGetLastError());
     return 0;
 }

@@ -109,6 +109,8 @@ int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset);
 int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset);
 /* r2c split (real.c:108-132): Z rows of h complex -> X rows of 2h complex */
 int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist);
+/* the same split writing bins 0..h only: X rows of h+1 complex */
+int hsd_r2c_post_compact(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist);
 /* c2r pre-twiddle (real.c:169-179): X rows (>= h+1 complex) -> Zin rows of h complex */
 int hsd_c2r_pre(const void *X, const void *tw2, void *Zin, int h, int batch, long long xdist, long long zdist);
 /* convolution helpers (convolve.c:147-160) */

@@ -55,6 +55,7 @@ SIGNATURES = {
     "hsfft_exec_batched": (CI, [VP, VP, VP, CI]),
     "hsfft_exec_batched_host": (CI, [VP, VP, VP, CI]),
     "hsfft_r2c_batched": (CI, [VP, VP, VP, CI]),
+    "hsfft_r2c_batched_compact": (CI, [VP, VP, VP, CI]),
     "hsfft_c2r_batched": (CI, [VP, VP, VP, CI]),
     "hsfft_convolve_batched": (CI, [ctypes.c_char_p, ctypes.c_char_p, VP, CI, VP, CI, VP, CI]),
     "hsfft_fill_complex": (CI, [VP, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64]),
@@ -231,6 +232,11 @@ def exec_batched_host(plan, x, out=None):
 
 def r2c_batched(rplan, d_in, d_out, batch):
     return check(lib().hsfft_r2c_batched(rplan.ptr, VP(d_in.ptr), VP(d_out.ptr), batch), "r2c_batched")
+
+
+def r2c_batched_compact(rplan, d_in, d_out, batch):
+    return check(lib().hsfft_r2c_batched_compact(rplan.ptr, VP(d_in.ptr), VP(d_out.ptr), batch),
+                 "r2c_batched_compact")
 
 
 def c2r_batched(rplan, d_in, d_out, batch):

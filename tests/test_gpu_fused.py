@@ -140,3 +140,17 @@ def test_bluestein_row_looped_kernels(n, mask, t, monkeypatch):
         din.free()
         dout.free()
         p.close()
+
+
+@pytest.mark.parametrize("n,batch", [(8, 3), (1000, 5), (1 << 16, 4), (1 << 22, 2), (2 * 99991, 2)])
+def test_r2c_compact_bit_exact(n, batch):
+    """hsfft_r2c_batched_compact: bins 0..N/2 per row, bit-identical to the reference-layout
+    output's first N/2+1 bins (and so to the oracle)"""
+    x = T.real_input(n, 0xC0 ^ n, batch=batch).reshape(batch, n)
+    rp = hsfft.RealPlan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(batch * (n // 2 + 1) * 16)
+    hsfft.r2c_batched_compact(rp, din, dout, batch)
+    y = dout.to_array(np.complex128).reshape(batch, n // 2 + 1)
+    ref = T.oracle_r2c(x, 1).reshape(batch, n)
+    assert T.bits_equal(y, np.ascontiguousarray(ref[:, :n // 2 + 1]))
