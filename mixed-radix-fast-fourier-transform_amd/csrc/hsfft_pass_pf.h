@@ -317,9 +317,9 @@ inline kfn b512_fn(int sgn, int conj)
 /* the pipelined kernel for this pass, or nullptr (then hsfft_pass_r8.h's k_pass runs) */
 inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *threads, size_t *lds)
 {
-    /* bit0: first pass (default: 26.8 vs 28.0 ms per 4096 x 2^20), bit1: later [8,8,8] pass
-     * (opt-in: measured equal to k_pass_b512, 23.7 vs 23.5 ms) */
-    const int mask = env("HSFFT_PF", 1);
+    /* bit0: first pass (26.9 vs 28.0 ms per 4096 x 2^20), bit1: later [8,8,8] pass (23.2-23.9
+     * vs 23.5-24.2 ms for k_pass_b512 over five paired runs) */
+    const int mask = env("HSFFT_PF", 3);
     if (l->load_op != HS_LOAD_PLAIN || l->store_op != HS_STORE_PLAIN) return nullptr;
     if (l->sgn != 1 && l->sgn != -1) return nullptr;
     for (int s = 1; s < p->nst; s++)
