@@ -194,7 +194,8 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
 /* ------------------------------------------------------------------ later pass [8,8,8]
  * P = 512 at L = B (A == 1): input [t][q] (t < 512, q < B), output [u][q].  A workgroup
  * owns 8 adjacent q-columns (128-B rows) and walks T rows of the batch; all three stages'
- * twiddles (k = q + B*kloc) are row-independent and stay in registers. */
+ * twiddles (k = q + B*kloc) are row-independent: stages 0/1 as LDS runs, stage 2 in
+ * registers.  Row prefetch (PREF) is opt-in: it costs the VGPRs that make the kernel spill. */
 /* stages + exchanges + store of one [8,8,8] tile-row; ocol = output row + q */
 template <int SGN>
 __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], const double2 (&w2)[7], double2 *lds,
@@ -216,7 +217,7 @@ __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], cons
     for (int jj = 0; jj < 8; jj++) stg(orow + (size_t)jj * TPG * B, lane, make_double2(xr[jj], xi[jj]));
 }
 
-template <int T, int SGN, bool CONJ>
+template <int T, int SGN, bool CONJ, bool PREF = true>
 __global__ __launch_bounds__(512, 4) void k_b512(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     const unsigned b0 = bg * T, nb = (unsigned)a.batch;
 
     double pr[8], pi[8];
-    {
+    if constexpr (PREF) {
         const double2 *row = a.in + (long long)b0 * a.idist;
         const unsigned lane = ((tid0 / G) * B + q0 + tid0 % G) * 16u;
 #pragma unroll
@@ -263,6 +264,25 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     __syncthreads();
 
     const int nit = (int)min((unsigned)T, nb - b0);
+    if constexpr (!PREF) { /* no row prefetch: 32 fewer VGPRs (no scratch spill) */
+#pragma unroll 1
+        for (int it = 0; it < nit; it++) {
+            unsigned tid = tid0;
+            asm volatile("" : "+v"(tid));
+            const unsigned g = tid % G, jt = tid / G;
+            const unsigned b = b0 + it, lane = (jt * B + q0 + g) * 16u;
+            const double2 *row = a.in + (long long)b * a.idist;
+            double xr[8], xi[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const double2 v = ldg(row + (size_t)i * TPG * B, lane);
+                xr[i] = v.x;
+                xi[i] = v.y;
+            }
+            b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
+        }
+        return;
+    }
 #pragma unroll 1
     for (int it = 0; it < nit - 1; it++) {
         unsigned tid = tid0;
@@ -310,6 +330,12 @@ inline kfn first_fn(int sgn, int conj)
 template <int T>
 inline kfn b512_fn(int sgn, int conj)
 {
+    /* default: no row prefetch -- 106 VGPRs, no scratch; 22.8 vs 23.4 ms with the prefetch
+     * (128 VGPRs + 40 B spill), i.e. the pass runs at the stream-copy rate */
+    if (!env("HSFFT_PFB_PREF", 0)) {
+        if (sgn == 1) return conj ? k_b512<T, 1, true, false> : k_b512<T, 1, false, false>;
+        return conj ? k_b512<T, -1, true, false> : k_b512<T, -1, false, false>;
+    }
     if (sgn == 1) return conj ? k_b512<T, 1, true> : k_b512<T, 1, false>;
     return conj ? k_b512<T, -1, true> : k_b512<T, -1, false>;
 }
