@@ -191,6 +191,74 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
     }
 }
 
+/* ------------------------------------------------------------------ first pass, 64-B loads
+ * Same [R0, 8^N8] first pass and the same G = 2 compute as k_first, but the column reads are
+ * 64-B segments: a workgroup owns 4 adjacent columns m0..m0+3 (two G = 2 tiles) and the four
+ * lanes of a DPP quad (threads jt, jt+1, each with h = 0/1) load one row segment per
+ * instruction: load A gives the even pair its own tile-0 values (row jt) and the odd pair the
+ * even pair's tile-1 values; load B the other way round (row jt+1).  A quad_perm swap
+ * returns the borrowed values.  k_first's 32-B segments cost one L2 request per 32 B, and
+ * that request rate, not HBM, is what holds it below the copy rate (TA stalled by TC). */
+__device__ __forceinline__ double quad_swap(double v)
+{
+    int2 u;
+    __builtin_memcpy(&u, &v, 8);
+    u.x = __builtin_amdgcn_mov_dpp(u.x, 0x4E, 0xF, 0xF, false); /* quad_perm [2,3,0,1] */
+    u.y = __builtin_amdgcn_mov_dpp(u.y, 0x4E, 0xF, 0xF, false);
+    double r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+}
+
+template <int R0, int N8, int SGN, bool CONJ>
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * 2), 4) void k_firstq(Args a)
+{
+    using S = Shape<R0, N8>;
+    constexpr int P = S::P, TPG = S::TPG, NT = TPG * 2, NB = 8 / R0, S0 = P / R0;
+    static_assert(N8 >= 1 && TPG % 2 == 0, "quad loads pair adjacent threads");
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    double2 *ltw = lds + P; /* after the G = 2 split image (P * 2 doubles) */
+    const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
+    const unsigned groups = (unsigned)a.tiles_q; /* 4-column groups per row */
+    const unsigned b = blk / groups, sg = blk % groups;
+    const unsigned A = (unsigned)a.A, nsup = A / 4;
+    const double2 *row = a.in + (long long)b * a.idist;
+    double2 *orow = a.out + (long long)b * a.odist;
+#pragma unroll 1
+    for (int i = threadIdx.x; i < P - 1; i += NT) ltw[i] = a.tw[i];
+    __syncthreads();
+    const int nit = (int)((nsup - 1 - sg) / groups + 1);
+#pragma unroll 1
+    for (int it = 0; it < nit; it++) {
+        unsigned tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const unsigned h = tid & 1, jt = tid >> 1, odd = jt & 1;
+        const unsigned m0 = (sg + it * groups) * 4;
+        const unsigned offA = ((jt - odd) * A + m0 + h + 2 * odd) * 16u;
+        const unsigned offB = ((jt + 1 - odd) * A + m0 + h + 2 - 2 * odd) * 16u;
+        double2 va[8], vb[8];
+#pragma unroll
+        for (int c = 0; c < NB; c++)
+#pragma unroll
+            for (int i = 0; i < R0; i++) {
+                const double2 *rb = row + (size_t)(c * TPG + i * S0) * A;
+                va[c * R0 + i] = ldg(rb, offA);
+                vb[c * R0 + i] = ldg(rb, offB);
+            }
+        double xr[8], xi[8], yr[8], yi[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const double2 own = odd ? vb[k] : va[k], oth = odd ? va[k] : vb[k];
+            xr[k] = own.x;
+            xi[k] = own.y;
+            yr[k] = quad_swap(oth.x);
+            yi[k] = quad_swap(oth.y);
+        }
+        first_body<R0, N8, 2, SGN, CONJ>(xr, xi, lds, ltw, orow, m0 + h, jt, h);
+        first_body<R0, N8, 2, SGN, CONJ>(yr, yi, lds, ltw, orow, m0 + 2 + h, jt, h);
+    }
+}
+
 /* ------------------------------------------------------------------ later pass [8,8,8]
  * P = 512 at L = B (A == 1): input [t][q] (t < 512, q < B), output [u][q].  A workgroup
  * owns 8 adjacent q-columns (128-B rows) and walks T rows of the batch; all three stages'
@@ -351,6 +419,17 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
     for (int s = 1; s < p->nst; s++)
         if (p->radix[s] != 8) return nullptr;
     if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 4) { /* 2^20's pass A: [4,8,8,8] */
+        /* default k_firstq walking 4 column groups: 24.0-24.3 ms per 4096 x 2^20 against
+         * 27.0-27.2 for k_first<G=2,T=2> (HSFFT_PFQ=0 selects k_first) */
+        const int q = env("HSFFT_PFQ", 4);
+        if (q > 0 && p->A % 4 == 0) { /* 64-B loads: *G = 4 columns per tile for the grid */
+            *G = 4;
+            *TL = q;
+            *threads = 512;
+            *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
+            if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 1, true> : k_firstq<4, 3, 1, false>;
+            return l->conj ? k_firstq<4, 3, -1, true> : k_firstq<4, 3, -1, false>;
+        }
         const int g = env("HSFFT_PFG", 2), t = env("HSFFT_PFT", 2); /* T=2: same time as 8, fabric reads 73.6 vs 103 GB */
         if (p->A % g) return nullptr;
         *threads = 256 * g;

@@ -1,6 +1,7 @@
 """GPU parity of the 2^20 hot-path kernel families (BASELINE config 2) against the oracle:
 
-* pf::k_first / pf::k_b512 (csrc/hsfft_pass_pf.h): software-pipelined two-launch passes;
+* pf::k_firstq / pf::k_first / pf::k_b512 (csrc/hsfft_pass_pf.h): the two-launch passes
+  (64-B quad-load first pass, its 32-B predecessor, the row-looped later pass);
 * fz::k_fused (csrc/hsfft_fused.h): both passes in one persistent launch with the
   intermediate handed over inside the launch (HSFFT_FUSED=1).
 
@@ -53,9 +54,10 @@ def _oracle(x, sgn, key):
     return _cache[k]
 
 
-@pytest.mark.parametrize("pf", ["0", "1", "2", "3"])
-def test_pipelined_passes_bit_exact(pf, monkeypatch):
+@pytest.mark.parametrize("pf,pfq", [("0", "4"), ("1", "4"), ("2", "4"), ("3", "4"), ("3", "0")])
+def test_pipelined_passes_bit_exact(pf, pfq, monkeypatch):
     monkeypatch.setenv("HSFFT_PF", pf)
+    monkeypatch.setenv("HSFFT_PFQ", pfq)
     x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
     for sgn in (1, -1):
         assert T.bits_equal(_run(x, sgn), _oracle(x, sgn, "b3")), (pf, sgn)
@@ -64,10 +66,22 @@ def test_pipelined_passes_bit_exact(pf, monkeypatch):
 @pytest.mark.parametrize("g,t", [(1, 8), (2, 2), (2, 8), (4, 4)])
 def test_pipelined_first_pass_tiles(g, t, monkeypatch):
     monkeypatch.setenv("HSFFT_PF", "1")
+    monkeypatch.setenv("HSFFT_PFQ", "0")
     monkeypatch.setenv("HSFFT_PFG", str(g))
     monkeypatch.setenv("HSFFT_PFT", str(t))
     x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
     assert T.bits_equal(_run(x, 1), _oracle(x, 1, "b3"))
+
+
+@pytest.mark.parametrize("q", ["1", "2", "3"])
+def test_quad_load_first_pass(q, monkeypatch):
+    """pf::k_firstq (64-B column loads, DPP quad swap): bit-exact, both signs, with a
+    4-column-group count per row (128) that is not a multiple of 3."""
+    monkeypatch.setenv("HSFFT_PF", "1")
+    monkeypatch.setenv("HSFFT_PFQ", q)
+    x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
+    for sgn in (1, -1):
+        assert T.bits_equal(_run(x, sgn), _oracle(x, sgn, "b3")), (q, sgn)
 
 
 @pytest.mark.parametrize("batch,r,lag", [(1, 2, 2), (2, 2, 2), (6, 2, 2), (8, 4, 1), (5, 1, 3), (6, 2, 9)])

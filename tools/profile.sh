@@ -12,6 +12,6 @@ SETS=${COUNTER_SETS:-"FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum|SQ_LDS_BANK
 IFS='|' read -ra SETARR <<< "$SETS"
 for set in "${SETARR[@]}"; do
   n=$(echo $set | tr ' ' '_' | cut -c1-40)
-  timeout -k 10 150 rocprofv3 --pmc $set -d $out/pmc_$n -o pmc --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > $out/pmc_$n.log 2>&1; rc=$?; echo "pmc $n rc=$rc"; stop $rc
+  timeout -s KILL 150 rocprofv3 --pmc $set -d $out/pmc_$n -o pmc --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > $out/pmc_$n.log 2>&1; rc=$?; echo "pmc $n rc=$rc"; stop $rc
 done
 exit 0
