@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Write profiles/pmc_traffic.json's entry for one bench config from a tools/prof_summary.py
+JSON: the dominant kernel (`--kernel` substring) and the other kernels with HBM bytes.
+Usage: tools/update_traffic.py <summary.json> <config> <kernel-substring> <batch> <algorithmic bytes>
+       <source file> <profile tag>"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    summ, cfg, ksub, batch, alg, source, tag = sys.argv[1:8]
+    s = json.load(open(summ))
+    dom = [k for k in s if ksub in k and "hbm_bytes_corrected" in s[k]]
+    if len(dom) != 1:
+        sys.exit(f"kernel substring {ksub!r} matches {dom}")
+    k = dom[0]
+    e = s[k]
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    cur = json.load(open(path)) if os.path.exists(path) else {}
+    cur[cfg] = {
+        "kernel": k,
+        "batch": int(batch),
+        "hbm_bytes_per_launch": int(e["hbm_bytes_corrected"]),
+        "fetch_size_kib": e["FETCH_SIZE"],
+        "write_size_kib": e["WRITE_SIZE"],
+        "avg_ms": e["avg_ms"],
+        "algorithmic_bytes_per_launch": int(alg),
+        "other_kernels": {o: {"hbm_bytes_per_launch": int(v["hbm_bytes_corrected"]), "avg_ms": v.get("avg_ms")}
+                          for o, v in s.items() if o != k and "hbm_bytes_corrected" in v and v.get("calls", 0) > 1},
+        "method": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of `python3 bench.py "
+                  f"--no-cpu-baseline` (tools/profile.sh {tag}); bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
+                  "(gfx950 FETCH_SIZE reports half of a wide streaming read, MI355X_MICROARCH.md HBM section); "
+                  "FETCH/WRITE count L2<->fabric traffic with Infinity Cache hits included",
+        "source": source,
+    }
+    json.dump(cur, open(path, "w"), indent=1)
+    print(json.dumps(cur[cfg], indent=1))
+
+
+if __name__ == "__main__":
+    main()
