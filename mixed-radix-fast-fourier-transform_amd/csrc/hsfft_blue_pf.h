@@ -142,9 +142,11 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
     const unsigned b0 = bg * T, nb = (unsigned)a.batch;
     const double2 *hk = a.saux;
 
+    double2 *itw = ltw + 504; /* tw[0, 511): the inverse first pass's stages L = 8, 64 */
     double2 w2[7];
     r8::load_tw_co<64>(w2, a, tid0 / G, q0);
     runs_to_lds<false>(ltw, a.tw, B, q0, tid0);
+    if (tid0 < 511) itw[tid0] = a.tw[tid0];
     r8::redistribute_tw(w2, lds);
     __syncthreads();
 
@@ -184,10 +186,10 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
          * small tables are cache-resident and nothing else is in flight here) */
         pf::stage<8, -S>(xr, xi, w, true);
         r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
-        pf::tw8<true>(w, a.tw, 8, jt & 7);
+        pf::tw8_lds<true>(w, itw, 8, jt & 7);
         pf::stage<8, -S>(xr, xi, w, false);
         r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
-        pf::tw8<true>(w, a.tw, 64, jt & 63);
+        pf::tw8_lds<true>(w, itw, 64, jt & 63);
         pf::stage<8, -S>(xr, xi, w, false);
         double2 *orow = a.out + (long long)(b0 + it) * a.odist;
 #pragma unroll
@@ -196,9 +198,9 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
 }
 
 /* Inverse FFT's second pass [8,8,8] at L = B = 512 (sign -S, conjugated twiddles) of q-tile
- * q0 for T rows, stored through the chirp for n < nsig (direction S).  Row prefetch as
- * pf::k_b512. */
-template <int T, int S>
+ * q0 for T rows, stored through the chirp for n < nsig (direction S).  Row prefetch (PREF)
+ * is opt-in (HSFFT_BLUE_PREF=1), as for pf::k_b512: with it the kernel spills 20 B. */
+template <int T, int S, bool PREF = true>
 __global__ __launch_bounds__(512, 4) void k_blast(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(512, 4) void k_blast(Args a)
     const unsigned nsig = (unsigned)a.nsig;
 
     double pr[8], pi[8];
-    {
+    if constexpr (PREF) {
         const double2 *row = a.in + (long long)b0 * a.idist;
         const unsigned lane = ((tid0 / G) * B + q0 + tid0 % G) * 16u;
 #pragma unroll
@@ -239,20 +241,32 @@ __global__ __launch_bounds__(512, 4) void k_blast(Args a)
         const unsigned g = tid % G, jt = tid / G, q = q0 + g;
         const unsigned lane = (jt * B + q) * 16u;
         double xr[8], xi[8];
+        if constexpr (PREF) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            xr[i] = pr[i];
-            xi[i] = pi[i];
+            for (int i = 0; i < 8; i++) {
+                xr[i] = pr[i];
+                xi[i] = pi[i];
+            }
+        } else {
+            const double2 *rowc = a.in + (long long)(b0 + it) * a.idist;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const double2 v = pf::ldg(rowc + (size_t)i * TPG * B, lane);
+                xr[i] = v.x;
+                xi[i] = v.y;
+            }
         }
         /* next row's loads (the last iteration re-reads its own row: no branch around the
          * loads, so nothing in the loop drains vmcnt early) */
-        const unsigned bn = it + 1 < nit ? b0 + it + 1 : b0 + it;
-        const double2 *rown = a.in + (long long)bn * a.idist;
+        if constexpr (PREF) {
+            const unsigned bn = it + 1 < nit ? b0 + it + 1 : b0 + it;
+            const double2 *rown = a.in + (long long)bn * a.idist;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const double2 v = pf::ldg(rown + (size_t)i * TPG * B, lane);
-            pr[i] = v.x;
-            pi[i] = v.y;
+            for (int i = 0; i < 8; i++) {
+                const double2 v = pf::ldg(rown + (size_t)i * TPG * B, lane);
+                pr[i] = v.x;
+                pi[i] = v.y;
+            }
         }
         double2 w[7];
 #pragma unroll
@@ -298,6 +312,8 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     else if (which == 0)
         fn = sgn == 1 ? (T == 8 ? k_bmid<8, 1> : T == 4 ? k_bmid<4, 1> : T == 2 ? k_bmid<2, 1> : k_bmid<1, 1>)
                       : (T == 8 ? k_bmid<8, -1> : T == 4 ? k_bmid<4, -1> : T == 2 ? k_bmid<2, -1> : k_bmid<1, -1>);
+    else if (T == 8 && !env("HSFFT_BLUE_PREF", 0)) /* c4: 20.98 vs 20.26 GS/s with the prefetch (spills) */
+        fn = sgn == 1 ? k_blast<8, 1, false> : k_blast<8, -1, false>;
     else
         fn = sgn == 1 ? (T == 8 ? k_blast<8, 1> : T == 4 ? k_blast<4, 1> : T == 2 ? k_blast<2, 1> : k_blast<1, 1>)
                       : (T == 8 ? k_blast<8, -1> : T == 4 ? k_blast<4, -1> : T == 2 ? k_blast<2, -1> : k_blast<1, -1>);
@@ -317,7 +333,8 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     a.tiles = a.tiles_q = 512 / 8;
     const long long grid = a.tiles * ((batch + T - 1) / T);
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
-    const size_t lds = (size_t)(512 * 8 + 512) * sizeof(double2); /* image + twiddle runs (k_bfirst: 511) */
+    /* image + twiddle runs (k_bfirst: 511; k_bmid: 504 forward runs + 511 inverse entries) */
+    const size_t lds = (size_t)(512 * 8 + (which == 0 ? 1016 : 512)) * sizeof(double2);
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a);
     HCHK(hipGetLastError());

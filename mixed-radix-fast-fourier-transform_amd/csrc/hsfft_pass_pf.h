@@ -100,10 +100,13 @@ __device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, uns
 }
 
 /* stages + exchanges + store of one first-pass tile held in xr/xi; ocol = output column */
-template <int R0, int N8, int G, int SGN, bool CONJ, bool SC1 = false>
+template <int R0, int N8, int G, int SGN, bool CONJ, bool SC1 = false, bool TWG = false>
 __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], double2 *lds, const double2 *ltw,
-                                           double2 *orow, unsigned m, unsigned jt, unsigned g)
+                                           double2 *orow, unsigned m, unsigned jt, unsigned g,
+                                           const double2 *gtw = nullptr)
 {
+    /* TWG: the third combine stage's twiddles come from the plan's table in global memory
+     * (L2-resident) instead of the LDS copy, so P = 4096 keeps an 8 KiB LDS table */
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG;
     double2 w[7];
@@ -119,8 +122,9 @@ __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], dou
         stage<8, SGN>(xr, xi, w, false);
     }
     if constexpr (N8 >= 3) {
+        if constexpr (TWG) tw8<CONJ>(w, gtw, S::Lloc(3), jt & (S::Lloc(3) - 1));
         r8::exchange<8, S::Lloc(2), 8, TPG, P, G, true>(xr, xi, lds, jt, g);
-        tw8_lds<CONJ>(w, ltw, S::Lloc(3), jt & (S::Lloc(3) - 1));
+        if constexpr (!TWG) tw8_lds<CONJ>(w, ltw, S::Lloc(3), jt & (S::Lloc(3) - 1));
         stage<8, SGN>(xr, xi, w, false);
     }
     /* last stage: output u = jt + jj*LL of the column, written to [m][u] */
@@ -191,51 +195,57 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
     }
 }
 
-/* ------------------------------------------------------------------ first pass, 64-B loads
- * Same [R0, 8^N8] first pass and the same G = 2 compute as k_first, but the column reads are
- * 64-B segments: a workgroup owns 4 adjacent columns m0..m0+3 (two G = 2 tiles) and the four
- * lanes of a DPP quad (threads jt, jt+1, each with h = 0/1) load one row segment per
- * instruction: load A gives the even pair its own tile-0 values (row jt) and the odd pair the
- * even pair's tile-1 values; load B the other way round (row jt+1).  A quad_perm swap
- * returns the borrowed values.  k_first's 32-B segments cost one L2 request per 32 B, and
- * that request rate, not HBM, is what holds it below the copy rate (TA stalled by TC). */
-__device__ __forceinline__ double quad_swap(double v)
+/* ------------------------------------------------------------------ first pass, paired loads
+ * Same [R0, 8^N8] first pass and the same G-column compute as k_first, but every column read
+ * is a 2G-column row segment (G = 2: 64 B, G = 1: 32 B): a workgroup owns 2G adjacent
+ * columns m0.. (two G-column tiles), and the 2G lanes of threads jt, jt+1 (even / odd, each
+ * with h < G) load one row segment per instruction: load A gives the even thread its own
+ * tile-0 values (row jt) and the odd thread the even one's tile-1 values; load B the other
+ * way round (row jt+1).  A DPP swap (lanes G apart inside a quad) returns the borrowed values.
+ * k_first's G-column segments cost one L2 request per 16 G bytes, and that request rate, not
+ * HBM, is what holds it below the copy rate (TA stalled by TC). */
+template <int G>
+__device__ __forceinline__ double pair_swap(double v)
 {
+    constexpr int CTRL = G == 2 ? 0x4E : 0xB1; /* quad_perm [2,3,0,1] / [1,0,3,2] */
     int2 u;
     __builtin_memcpy(&u, &v, 8);
-    u.x = __builtin_amdgcn_mov_dpp(u.x, 0x4E, 0xF, 0xF, false); /* quad_perm [2,3,0,1] */
-    u.y = __builtin_amdgcn_mov_dpp(u.y, 0x4E, 0xF, 0xF, false);
+    u.x = __builtin_amdgcn_mov_dpp(u.x, CTRL, 0xF, 0xF, false);
+    u.y = __builtin_amdgcn_mov_dpp(u.y, CTRL, 0xF, 0xF, false);
     double r;
     __builtin_memcpy(&r, &u, 8);
     return r;
 }
 
-template <int R0, int N8, int SGN, bool CONJ>
-__global__ __launch_bounds__((Shape<R0, N8>::TPG * 2), 4) void k_firstq(Args a)
+template <int R0, int N8, int G, int SGN, bool CONJ>
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
 {
     using S = Shape<R0, N8>;
-    constexpr int P = S::P, TPG = S::TPG, NT = TPG * 2, NB = 8 / R0, S0 = P / R0;
-    static_assert(N8 >= 1 && TPG % 2 == 0, "quad loads pair adjacent threads");
+    constexpr int P = S::P, TPG = S::TPG, NT = TPG * G, NB = 8 / R0, S0 = P / R0;
+    /* P = 4096: the L = 512 stage's twiddles from global memory (LDS: 32 + 8 KiB) */
+    constexpr bool TWG = N8 >= 3 && P > 2048;
+    constexpr int NTAB = TWG ? S::Lloc(3) - 1 : P - 1;
+    static_assert((G == 1 || G == 2) && N8 >= 1 && TPG % 2 == 0, "paired loads");
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    double2 *ltw = lds + P; /* after the G = 2 split image (P * 2 doubles) */
+    double2 *ltw = lds + P * G / 2; /* after the split image (P * G doubles) */
     const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
-    const unsigned groups = (unsigned)a.tiles_q; /* 4-column groups per row */
+    const unsigned groups = (unsigned)a.tiles_q; /* 2G-column groups per row */
     const unsigned b = blk / groups, sg = blk % groups;
-    const unsigned A = (unsigned)a.A, nsup = A / 4;
+    const unsigned A = (unsigned)a.A, nsup = A / (2 * G);
     const double2 *row = a.in + (long long)b * a.idist;
     double2 *orow = a.out + (long long)b * a.odist;
 #pragma unroll 1
-    for (int i = threadIdx.x; i < P - 1; i += NT) ltw[i] = a.tw[i];
+    for (int i = threadIdx.x; i < NTAB; i += NT) ltw[i] = a.tw[i];
     __syncthreads();
     const int nit = (int)((nsup - 1 - sg) / groups + 1);
 #pragma unroll 1
     for (int it = 0; it < nit; it++) {
         unsigned tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
-        const unsigned h = tid & 1, jt = tid >> 1, odd = jt & 1;
-        const unsigned m0 = (sg + it * groups) * 4;
-        const unsigned offA = ((jt - odd) * A + m0 + h + 2 * odd) * 16u;
-        const unsigned offB = ((jt + 1 - odd) * A + m0 + h + 2 - 2 * odd) * 16u;
+        const unsigned h = tid % G, jt = tid / G, odd = jt & 1;
+        const unsigned m0 = (sg + it * groups) * (2 * G);
+        const unsigned offA = ((jt - odd) * A + m0 + h + G * odd) * 16u;
+        const unsigned offB = ((jt + 1 - odd) * A + m0 + h + G - G * odd) * 16u;
         double2 va[8], vb[8];
 #pragma unroll
         for (int c = 0; c < NB; c++)
@@ -251,11 +261,11 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * 2), 4) void k_firstq(Args a)
             const double2 own = odd ? vb[k] : va[k], oth = odd ? va[k] : vb[k];
             xr[k] = own.x;
             xi[k] = own.y;
-            yr[k] = quad_swap(oth.x);
-            yi[k] = quad_swap(oth.y);
+            yr[k] = pair_swap<G>(oth.x);
+            yi[k] = pair_swap<G>(oth.y);
         }
-        first_body<R0, N8, 2, SGN, CONJ>(xr, xi, lds, ltw, orow, m0 + h, jt, h);
-        first_body<R0, N8, 2, SGN, CONJ>(yr, yi, lds, ltw, orow, m0 + 2 + h, jt, h);
+        first_body<R0, N8, G, SGN, CONJ, false, TWG>(xr, xi, lds, ltw, orow, m0 + h, jt, h, a.tw);
+        first_body<R0, N8, G, SGN, CONJ, false, TWG>(yr, yi, lds, ltw, orow, m0 + G + h, jt, h, a.tw);
     }
 }
 
@@ -427,8 +437,8 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = q;
             *threads = 512;
             *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
-            if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 1, true> : k_firstq<4, 3, 1, false>;
-            return l->conj ? k_firstq<4, 3, -1, true> : k_firstq<4, 3, -1, false>;
+            if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 2, 1, true> : k_firstq<4, 3, 2, 1, false>;
+            return l->conj ? k_firstq<4, 3, 2, -1, true> : k_firstq<4, 3, 2, -1, false>;
         }
         const int g = env("HSFFT_PFG", 2), t = env("HSFFT_PFT", 2); /* T=2: same time as 8, fabric reads 73.6 vs 103 GB */
         if (p->A % g) return nullptr;
@@ -447,6 +457,19 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
         return *TL == 4 ? first_fn<4, 3, 4, 4>(l->sgn, l->conj)
              : *TL == 2 ? first_fn<4, 3, 4, 2>(l->sgn, l->conj)
                         : first_fn<4, 3, 4, 1>(l->sgn, l->conj);
+    }
+    if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 8 && p->A % 2 == 0) {
+        /* [8,8,8,8] first pass (2^21 = r2c 2^22's inner pass A): 32-B paired loads, one column
+         * per thread group, L = 512 twiddles from global memory */
+        const int q = env("HSFFT_PFP", 4);
+        if (q > 0) {
+            *G = 2; /* columns per tile group, for the grid */
+            *TL = q;
+            *threads = 512;
+            *lds = (size_t)4096 * sizeof(double) + 511 * sizeof(double2);
+            if (l->sgn == 1) return l->conj ? k_firstq<8, 3, 1, 1, true> : k_firstq<8, 3, 1, 1, false>;
+            return l->conj ? k_firstq<8, 3, 1, -1, true> : k_firstq<8, 3, 1, -1, false>;
+        }
     }
     if ((mask & 2) && p->B > 1 && p->nst == 3 && p->radix[0] == 8 && p->A == 1 && p->B % 8 == 0) {
         const int t = env("HSFFT_PFB", 8);

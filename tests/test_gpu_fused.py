@@ -84,6 +84,26 @@ def test_quad_load_first_pass(q, monkeypatch):
         assert T.bits_equal(_run(x, sgn), _oracle(x, sgn, "b3")), (q, sgn)
 
 
+@pytest.mark.parametrize("pfp", ["0", "1", "4"])
+def test_paired_load_first_pass_2p21(pfp, monkeypatch):
+    """pf::k_firstq<8,3,G=1> (2^21 = [8,8,8,8 | 8,8,8], r2c 2^22's inner c2c): 32-B paired
+    column loads, L = 512 twiddles from global memory; bit-exact, both signs, odd batch."""
+    monkeypatch.setenv("HSFFT_PFP", pfp)
+    n = 1 << 21
+    x = T.complex_input(n, 0x2121, batch=3).reshape(3, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, 3)
+        hsfft.synchronize()
+        y = dout.to_array(np.complex128).reshape(3, n)
+        assert T.bits_equal(y, _oracle(x, sgn, "2p21")), (pfp, sgn)
+        din.free()
+        dout.free()
+        p.close()
+
+
 @pytest.mark.parametrize("batch,r,lag", [(1, 2, 2), (2, 2, 2), (6, 2, 2), (8, 4, 1), (5, 1, 3), (6, 2, 9)])
 def test_fused_bit_exact(batch, r, lag, monkeypatch):
     monkeypatch.setenv("HSFFT_FUSED", "1")
@@ -134,14 +154,16 @@ def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("mask,t", [("0", "4"), ("3", "1"), ("3", "2"), ("3", "4"), ("3", "8"), ("1", "4"), ("2", "4")])
+@pytest.mark.parametrize("mask,t,pref", [("0", "4", "0"), ("3", "1", "0"), ("3", "2", "0"), ("3", "4", "0"), ("3", "8", "0"),
+                                         ("7", "8", "1"), ("1", "4", "0"), ("2", "4", "0")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
-def test_bluestein_row_looped_kernels(n, mask, t, monkeypatch):
+def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
     """Bluestein with M = 2^18 (config 4's size; 65537 = 2^16+1 is the plan/exec M mismatch
     case D5, computed with its own exec-length table): the row-looped middle / last kernels
     (csrc/hsfft_blue_pf.h) for every tile-row count, odd batch, both signs, bit-exact."""
     monkeypatch.setenv("HSFFT_BLUE_PF", mask)
     monkeypatch.setenv("HSFFT_BLUE_T", t)
+    monkeypatch.setenv("HSFFT_BLUE_PREF", pref)
     x = T.complex_input(n, 0xB1 ^ n, batch=5).reshape(5, n)
     for sgn in (1, -1):
         p = hsfft.Plan(n, sgn)
