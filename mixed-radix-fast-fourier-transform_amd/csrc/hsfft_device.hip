@@ -568,7 +568,10 @@ int hsd_fused20(const void *in, long long idist, void *out, long long odist, con
         HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 16 * sizeof(unsigned), stream()));
         a.dbg = s_dbg;
     }
-    fz::ffn fn = R == 1 ? fz::fused_fn<1>(sgn, conj) : R == 2 ? fz::fused_fn<2>(sgn, conj) : fz::fused_fn<4>(sgn, conj);
+    const char *qe = getenv("HSFFT_FZ_Q"); /* pass-A items with 64-B paired loads (default) */
+    const bool qa = !(qe && atoi(qe) == 0);
+    fz::ffn fn = R == 1 ? fz::fused_fn<1>(sgn, conj, qa) : R == 2 ? fz::fused_fn<2>(sgn, conj, qa)
+                                                                 : fz::fused_fn<4>(sgn, conj, qa);
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fz::LDS_BYTES));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), fz::LDS_BYTES, stream(), a);
     HCHK(hipGetLastError());

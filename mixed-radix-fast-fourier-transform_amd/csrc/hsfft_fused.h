@@ -150,6 +150,46 @@ __device__ __forceinline__ void a_item2(const FArgs &a, unsigned row, unsigned t
     pf::first_body<4, 3, G, SGN, CONJ, true>(pr, pi, lds, ltw, orow, tb * G + g0, jt0, g0);
 }
 
+/* pass A, one 4-column group m0 .. m0+3 of `row` (two 2-column tiles) with the 64-B paired
+ * loads of pf::k_firstq, results stored write-through (sc1) */
+template <int SGN, bool CONJ>
+__device__ __forceinline__ void a_itemq(const FArgs &a, unsigned row, unsigned m0, double2 *lds, unsigned tid)
+{
+    constexpr int P = 2048, TPG = 256;
+    double2 *ltw = lds + 2048;
+    const double2 *in = a.in + (long long)row * a.idist;
+    double2 *orow = a.out + (long long)row * a.odist;
+    const unsigned h = tid & 1, jt = tid >> 1, odd = jt & 1;
+    const unsigned offA = ((jt - odd) * 512u + m0 + h + 2 * odd) * 16u;
+    const unsigned offB = ((jt + 1 - odd) * 512u + m0 + h + 2 - 2 * odd) * 16u;
+    double2 va[8], vb[8];
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const double2 *rb = in + (size_t)(c * TPG + i * (P / 4)) * 512;
+            va[c * 4 + i] = pf::ldg(rb, offA);
+            vb[c * 4 + i] = pf::ldg(rb, offB);
+        }
+#pragma unroll
+    for (int i = tid; i < P - 1; i += 512) ltw[i] = a.tw[i];
+    __syncthreads();
+    unsigned t = tid;
+    asm volatile("" : "+v"(t));
+    const unsigned hh = t & 1, jj = t >> 1;
+    double xr[8], xi[8], yr[8], yi[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const double2 own = odd ? vb[k] : va[k], oth = odd ? va[k] : vb[k];
+        xr[k] = own.x;
+        xi[k] = own.y;
+        yr[k] = pf::pair_swap<2>(oth.x);
+        yi[k] = pf::pair_swap<2>(oth.y);
+    }
+    pf::first_body<4, 3, 2, SGN, CONJ, true>(xr, xi, lds, ltw, orow, m0 + hh, jj, hh);
+    pf::first_body<4, 3, 2, SGN, CONJ, true>(yr, yi, lds, ltw, orow, m0 + 2 + hh, jj, hh);
+}
+
 /* pass B, one tile (q-columns 8*qt .. 8*qt+7) over the R rows of group grp, reading the
  * intermediate with sc1 loads; output written in place with plain stores */
 template <int R, int SGN, bool CONJ>
@@ -162,17 +202,6 @@ __device__ __forceinline__ void b_item(const FArgs &a, unsigned grp, unsigned qt
     const unsigned row0 = grp * R;
     const unsigned g0 = tid & 7, jt0 = tid >> 3;
     const unsigned lane0 = (jt0 * B + q0 + g0) * 16u;
-    double pr[8], pi[8];
-    {
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(a.out + (long long)row0 * a.odist, 0, (int)ROW_BYTES, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const double2 v = as_d2(__builtin_amdgcn_raw_buffer_load_b128(rs, lane0, i * TPG * B * 16, 16));
-            pr[i] = v.x;
-            pi[i] = v.y;
-        }
-    }
     /* twiddles: stage 2 in registers (coalesced run + redistribution through the image),
      * stages 0/1 as LDS runs (pf::k_b512 layout) */
     r8::Args ta;
@@ -193,29 +222,24 @@ __device__ __forceinline__ void b_item(const FArgs &a, unsigned grp, unsigned qt
         for (int i = 0; i < 7; i++) w2[i].y = -w2[i].y;
     }
     __syncthreads();
+    /* no row prefetch (as pf::k_b512's default): 32 fewer live VGPRs */
 #pragma unroll 1
-    for (int it = 0; it < R - 1; it++) {
+    for (int it = 0; it < R; it++) {
         unsigned t = tid;
         asm volatile("" : "+v"(t));
         const unsigned g = t & 7, jt = t >> 3;
         const unsigned lane = (jt * B + q0 + g) * 16u;
         double xr[8], xi[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            xr[i] = pr[i];
-            xi[i] = pi[i];
-        }
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            a.out + (long long)(row0 + it + 1) * a.odist, 0, (int)ROW_BYTES, 0x00020000);
+            a.out + (long long)(row0 + it) * a.odist, 0, (int)ROW_BYTES, 0x00020000);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const double2 v = as_d2(__builtin_amdgcn_raw_buffer_load_b128(rs, lane, i * TPG * B * 16, 16));
-            pr[i] = v.x;
-            pi[i] = v.y;
+            xr[i] = v.x;
+            xi[i] = v.y;
         }
         pf::b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)(row0 + it) * a.odist, B, lane, jt, g);
     }
-    pf::b512_body<SGN>(pr, pi, w2, lds, ltw, a.out + (long long)(row0 + R - 1) * a.odist, B, lane0, jt0, g0);
 }
 
 /* ticket t of a queue -> (pass, group, index within the group's slice of this queue) */
@@ -245,7 +269,7 @@ __device__ __forceinline__ void decode(unsigned t, unsigned ng, unsigned lag, bo
     i = t % nB;
 }
 
-template <int R, int SGN, bool CONJ>
+template <int R, int SGN, bool CONJ, bool QA = false>
 __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -287,7 +311,10 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
         const unsigned long long t_item = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
         if (isA) {
             const unsigned row = grp * R + i / (AQ / 2), k = i % (AQ / 2);
-            a_item2<SGN, CONJ>(a, row, x * AQ + k, x * AQ + k + AQ / 2, lds, tid);
+            if constexpr (QA) /* tiles 2k', 2k'+1 as one 4-column group (64-B loads) */
+                a_itemq<SGN, CONJ>(a, row, (x * AQ + 2 * k) * 2, lds, tid);
+            else
+                a_item2<SGN, CONJ>(a, row, x * AQ + k, x * AQ + k + AQ / 2, lds, tid);
             const unsigned long long t_st = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* every storing wave: payload landed */
             if (a.dbg && tid == 0) a.dbg[blockIdx.x * 16 + 10] += (unsigned)(__builtin_amdgcn_s_memrealtime() - t_st);
@@ -333,8 +360,12 @@ __global__ __launch_bounds__(512, 4) void k_fused(FArgs a)
 typedef void (*ffn)(FArgs);
 
 template <int R>
-inline ffn fused_fn(int sgn, int conj)
+inline ffn fused_fn(int sgn, int conj, bool qa)
 {
+    if (qa) {
+        if (sgn == 1) return conj ? k_fused<R, 1, true, true> : k_fused<R, 1, false, true>;
+        return conj ? k_fused<R, -1, true, true> : k_fused<R, -1, false, true>;
+    }
     if (sgn == 1) return conj ? k_fused<R, 1, true> : k_fused<R, 1, false>;
     return conj ? k_fused<R, -1, true> : k_fused<R, -1, false>;
 }
