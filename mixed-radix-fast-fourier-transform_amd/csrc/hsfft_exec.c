@@ -728,8 +728,8 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
 {
     const hsd_pass *p0 = &e->pass[0], *p1 = &e->pass[1];
     if (e->lt != 0 || e->npass != 2 || p1->variant != HS_KV_R8X3 || p1->nst != 3 || p1->P != 512 || p1->A != 1 ||
-        p1->B % 16 || p0->B != 1 || !env_int("HSFFT_R2C_FUSE", 0))
-        return 1; /* opt-in: measured no faster than pass B + k_r2c_post (register pressure) */
+        p1->B % 16 || p0->B != 1 || !env_int("HSFFT_R2C_FUSE", 1))
+        return 1; /* HSFFT_R2C_FUSE=0: pass B + k_r2c_post2 (r2c 2^22: 85 vs 93 GSamples/s fused) */
     hs_devstate *ds = devstate(e);
     if (!ds) return HSFFT_ERR_DEVICE;
     int rc = launch_pass(e, ds, 0, in, idist, Z, e->M, batch, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN,

@@ -389,6 +389,143 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     }
 }
 
+/* ------------------------------------------------------------------ r2c split in pass B
+ * real.c's split (ref :108-132) fused into the last [8,8,8] pass of the inner c2c of h = P*B
+ * points (2^21 for r2c 2^22): output k = u*B + q pairs with h - k = (P-1-u)*B + (B-q), so the
+ * q-columns [8j+1, 8j+9) ("lo") and [B-8j-8, B-8j) ("hi") are closed under the pairing.  A
+ * workgroup transforms both tiles (k_b512's stages: stage-0/1 twiddle runs in LDS, stage-2
+ * twiddles coalesced and redistributed), swaps the hi tile through LDS and writes X[k],
+ * X[N-k], X[h-k], X[h+k] of its lo tile.  Tile j == B/16 is column 0 (u <-> P-u, X[0], X[h]).
+ * Saves the c2c output's write and re-read (16 of 56 bytes per real sample). */
+template <int SGN>
+__device__ __forceinline__ void r2c_tile(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned B, unsigned q0,
+                                         const double2 *tw, double2 *lds, double2 *ltw, unsigned tid0)
+{
+    constexpr int TPG = 64, P = 512, G = 8;
+    const unsigned lane0 = ((tid0 >> 3) * B + q0 + (tid0 & 7)) * 16u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
+        xr[i] = v.x;
+        xi[i] = v.y;
+    }
+    r8::Args ta;
+    ta.tw = tw;
+    ta.B = B;
+    double2 w2[7];
+    r8::load_tw_co<64>(w2, ta, (int)(tid0 >> 3), q0);
+    __syncthreads(); /* earlier readers of the image and of ltw are done */
+    if (tid0 < 504) {
+        const unsigned r = tid0 / 56, e = tid0 % 56;
+        const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
+        ltw[tid0] = tw[src];
+    }
+    r8::redistribute_tw(w2, lds);
+    __syncthreads(); /* ltw written; every wave has read its redistributed twiddles back */
+    unsigned tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const unsigned g = tid & 7, jt = tid >> 3;
+    double2 w[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = ltw[7 * g + i];
+    stage<8, SGN>(xr, xi, w, false);
+    r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = ltw[56 * (1 + (jt & 7)) + 7 * g + i];
+    stage<8, SGN>(xr, xi, w, false);
+    r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    stage<8, SGN>(xr, xi, w2, false);
+}
+
+template <int SGN>
+__global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    double2 *ltw = lds + P * G;
+    const unsigned blk = xcd_remap(blockIdx.x);
+    const unsigned tiles = (unsigned)a.tiles, b = blk / tiles, j = blk % tiles;
+    const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
+    const double2 *row = a.in + (long long)b * a.idist;
+    double2 *X = a.out + (long long)b * a.odist;
+    const double2 *w2t = a.saux;
+    double xr[8], xi[8];
+    if (j < tiles - 1) {
+        const unsigned qlo = 8 * j + 1, qhi = B - 8 * j - 8;
+        double hr[8], hi[8];
+        r2c_tile<SGN>(hr, hi, row, B, qhi, a.tw, lds, ltw, tid0);
+        r2c_tile<SGN>(xr, xi, row, B, qlo, a.tw, lds, ltw, tid0);
+        __syncthreads();
+        const unsigned g = tid0 & 7, jt = tid0 >> 3;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(hr[jj], hi[jj]);
+        __syncthreads();
+        const unsigned q = qlo + g;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B + q, hk = h - k;
+            const double2 zk = make_double2(xr[jj], xi[jj]), zh = lds[(P - 1 - u) * G + (7 - g)];
+            double re, im;
+            r8::r2c_pair(zk, zh, w2t[k], re, im);
+            X[k] = make_double2(re, im);
+            X[N - k] = make_double2(re, -im);
+            r8::r2c_pair(zh, zk, w2t[hk], re, im);
+            X[hk] = make_double2(re, im);
+            X[N - hk] = make_double2(re, -im);
+        }
+    } else { /* column 0: k = u*B pairs with (P-u)*B */
+        r2c_tile<SGN>(xr, xi, row, B, 0, a.tw, lds, ltw, tid0);
+        __syncthreads();
+        const unsigned g = tid0 & 7, jt = tid0 >> 3;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B;
+            const double2 zk = make_double2(xr[jj], xi[jj]);
+            if (u == 0) {
+                X[0] = make_double2(zk.x + zk.y, 0.0);
+                X[h] = make_double2(zk.x - zk.y, 0.0);
+            } else {
+                const double2 zh = lds[(P - u) * G];
+                double re, im;
+                r8::r2c_pair(zk, zh, w2t[k], re, im);
+                X[k] = make_double2(re, im);
+                X[N - k] = make_double2(re, -im);
+            }
+        }
+    }
+}
+
+/* returns 1 if not applicable, 0 on launch, < 0 on error */
+inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2,
+                            long long h, long long B, int batch, int sgn, hipStream_t st)
+{
+    if (B % 16 || B * 512 != h || h > 0x40000000LL || (sgn != 1 && sgn != -1)) return 1;
+    Args a;
+    memset(&a, 0, sizeof a);
+    a.in = (const double2 *)Z;
+    a.out = (double2 *)X;
+    a.tw = (const double2 *)tw;
+    a.saux = (const double2 *)w2;
+    a.idist = zdist;
+    a.odist = xdist;
+    a.A = 1;
+    a.B = B;
+    a.batch = batch;
+    a.tiles = a.tiles_q = B / 16 + 1;
+    const long long grid = a.tiles * (long long)batch;
+    if (grid <= 0 || grid > 0x7fffffffLL) return -1;
+    const size_t lds = (size_t)(512 * 8 + 504) * sizeof(double2);
+    void (*fn)(Args, unsigned) = sgn == 1 ? k_r2c_fused<1> : k_r2c_fused<-1>;
+    HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a, (unsigned)h);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
 /* ------------------------------------------------------------------ host side */
 typedef void (*kfn)(Args);
 

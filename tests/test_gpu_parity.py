@@ -317,17 +317,19 @@ def test_two_pass_2pow21_batched():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1 << 19, 1 << 22])
-def test_r2c_fused_split_opt_in(n, monkeypatch):
-    """HSFFT_R2C_FUSE=1: the real.c split fused into the last c2c pass (k_r2c_last), bit-exact."""
-    monkeypatch.setenv("HSFFT_R2C_FUSE", "1")
-    x = T.real_input(n, 23, batch=2).reshape(2, n)
-    rp = hsfft.RealPlan(n, 1)
+@pytest.mark.parametrize("fuse", ["0", "1", "2"])
+@pytest.mark.parametrize("n,sgn", [(1 << 19, 1), (1 << 22, 1), (1 << 22, -1), (1 << 13, 1)])
+def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
+    """the real.c split fused into the last c2c pass (HSFFT_R2C_FUSE=1, default: pf::k_r2c_fused;
+    2: r8::k_r2c_last; 0: separate split kernel), bit-exact, both plan signs, odd batch."""
+    monkeypatch.setenv("HSFFT_R2C_FUSE", fuse)
+    x = T.real_input(n, 23, batch=3).reshape(3, n)
+    rp = hsfft.RealPlan(n, sgn)
     din = hsfft.DeviceBuffer.from_array(x)
-    dout = hsfft.DeviceBuffer(2 * n * 16)
-    hsfft.r2c_batched(rp, din, dout, 2)
-    y = dout.to_array(np.complex128).reshape(2, n)
-    assert T.bits_equal(y, T.oracle_r2c(x, 1))
+    dout = hsfft.DeviceBuffer(3 * n * 16)
+    hsfft.r2c_batched(rp, din, dout, 3)
+    y = dout.to_array(np.complex128).reshape(3, n)
+    assert T.bits_equal(y, T.oracle_r2c(x, sgn))
 
 
 def _full_size_c2c(n, batch, seed, rows, sgn=1, tol=1e-13, roundtrip=True, flags=0):
