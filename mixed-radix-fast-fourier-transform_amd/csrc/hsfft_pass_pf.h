@@ -397,11 +397,13 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
  * twiddles coalesced and redistributed), swaps the hi tile through LDS and writes X[k],
  * X[N-k], X[h-k], X[h+k] of its lo tile.  Tile j == B/16 is column 0 (u <-> P-u, X[0], X[h]).
  * Saves the c2c output's write and re-read (16 of 56 bytes per real sample). */
-template <int SGN>
-__device__ __forceinline__ void r2c_tile(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned B, unsigned q0,
-                                         const double2 *tw, double2 *lds, double2 *ltw, unsigned tid0)
+/* one tile's row loads, its stage-0/1 twiddle runs (-> ltw) and stage-2 twiddles (coalesced,
+ * redistributed through the image: every earlier reader of the image must be done) */
+__device__ __forceinline__ void r2c_load(double (&xr)[8], double (&xi)[8], double2 (&w2)[7], const double2 *row,
+                                         unsigned B, unsigned q0, const double2 *tw, double2 *lds, double2 *ltw,
+                                         unsigned tid0)
 {
-    constexpr int TPG = 64, P = 512, G = 8;
+    constexpr int TPG = 64;
     const unsigned lane0 = ((tid0 >> 3) * B + q0 + (tid0 & 7)) * 16u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -412,7 +414,6 @@ __device__ __forceinline__ void r2c_tile(double (&xr)[8], double (&xi)[8], const
     r8::Args ta;
     ta.tw = tw;
     ta.B = B;
-    double2 w2[7];
     r8::load_tw_co<64>(w2, ta, (int)(tid0 >> 3), q0);
     __syncthreads(); /* earlier readers of the image and of ltw are done */
     if (tid0 < 504) {
@@ -422,6 +423,14 @@ __device__ __forceinline__ void r2c_tile(double (&xr)[8], double (&xi)[8], const
     }
     r8::redistribute_tw(w2, lds);
     __syncthreads(); /* ltw written; every wave has read its redistributed twiddles back */
+}
+
+/* the tile's three stages; SPLIT: exchanges through doubles [0, 4096) only */
+template <int SGN, bool SPLIT>
+__device__ __forceinline__ void r2c_stages(double (&xr)[8], double (&xi)[8], const double2 (&w2)[7], double2 *lds,
+                                           const double2 *ltw, unsigned tid0)
+{
+    constexpr int TPG = 64, P = 512, G = 8;
     unsigned tid = tid0;
     asm volatile("" : "+v"(tid));
     const unsigned g = tid & 7, jt = tid >> 3;
@@ -429,11 +438,11 @@ __device__ __forceinline__ void r2c_tile(double (&xr)[8], double (&xi)[8], const
 #pragma unroll
     for (int i = 0; i < 7; i++) w[i] = ltw[7 * g + i];
     stage<8, SGN>(xr, xi, w, false);
-    r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    r8::exchange<8, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
 #pragma unroll
     for (int i = 0; i < 7; i++) w[i] = ltw[56 * (1 + (jt & 7)) + 7 * g + i];
     stage<8, SGN>(xr, xi, w, false);
-    r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+    r8::exchange<8, 8, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
     stage<8, SGN>(xr, xi, w2, false);
 }
 
@@ -443,6 +452,7 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
     constexpr int P = 512, TPG = 64, G = 8;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *ltw = lds + P * G;
+    double *ld = reinterpret_cast<double *>(lds); /* [0, 4096): split image / hi imag, [4096, 8192): hi real */
     const unsigned blk = xcd_remap(blockIdx.x);
     const unsigned tiles = (unsigned)a.tiles, b = blk / tiles, j = blk % tiles;
     const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
@@ -450,21 +460,29 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
     double2 *X = a.out + (long long)b * a.odist;
     const double2 *w2t = a.saux;
     double xr[8], xi[8];
+    double2 w2[7];
+    const unsigned g = tid0 & 7, jt = tid0 >> 3;
     if (j < tiles - 1) {
         const unsigned qlo = 8 * j + 1, qhi = B - 8 * j - 8;
         double hr[8], hi[8];
-        r2c_tile<SGN>(hr, hi, row, B, qhi, a.tw, lds, ltw, tid0);
-        r2c_tile<SGN>(xr, xi, row, B, qlo, a.tw, lds, ltw, tid0);
-        __syncthreads();
-        const unsigned g = tid0 & 7, jt = tid0 >> 3;
+        r2c_load(hr, hi, w2, row, B, qhi, a.tw, lds, ltw, tid0);
+        r2c_stages<SGN, false>(hr, hi, w2, lds, ltw, tid0);
+        r2c_load(xr, xi, w2, row, B, qlo, a.tw, lds, ltw, tid0);
+        /* the hi tile's real parts wait in the image's upper half (the lo tile's split
+         * exchanges use the lower half), so only its imaginary parts stay in registers */
 #pragma unroll
-        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(hr[jj], hi[jj]);
+        for (int jj = 0; jj < 8; jj++) ld[4096 + (jt + jj * TPG) * G + g] = hr[jj];
+        r2c_stages<SGN, true>(xr, xi, w2, lds, ltw, tid0);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = hi[jj];
         __syncthreads();
         const unsigned q = qlo + g;
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
             const unsigned u = jt + jj * TPG, k = u * B + q, hk = h - k;
-            const double2 zk = make_double2(xr[jj], xi[jj]), zh = lds[(P - 1 - u) * G + (7 - g)];
+            const unsigned s = (P - 1 - u) * G + (7 - g);
+            const double2 zk = make_double2(xr[jj], xi[jj]), zh = make_double2(ld[4096 + s], ld[s]);
             double re, im;
             r8::r2c_pair(zk, zh, w2t[k], re, im);
             X[k] = make_double2(re, im);
@@ -474,9 +492,9 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
             X[N - hk] = make_double2(re, -im);
         }
     } else { /* column 0: k = u*B pairs with (P-u)*B */
-        r2c_tile<SGN>(xr, xi, row, B, 0, a.tw, lds, ltw, tid0);
+        r2c_load(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
+        r2c_stages<SGN, false>(xr, xi, w2, lds, ltw, tid0);
         __syncthreads();
-        const unsigned g = tid0 & 7, jt = tid0 >> 3;
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
         __syncthreads();
