@@ -36,6 +36,7 @@ struct MArgs {
     long long idist, odist;
     int A, B, tiles_q, tiles, batch;
     int sgn, conj;
+    int xcd; /* XCD-aware block remap */
 };
 
 constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -121,7 +122,12 @@ __global__ __launch_bounds__(TPG * G) void k_pass(MArgs a)
     constexpr int NM = nmax<NST, R0, R1, R2, R3, TPG>();
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
 
-    const unsigned blk = blockIdx.x, tiles = (unsigned)a.tiles;
+    unsigned blk = blockIdx.x;
+    if (a.xcd) { /* consecutive tiles of a row on one XCD: they share the lines at tile edges */
+        const unsigned nwg = gridDim.x, q8 = nwg / 8, r8_ = nwg % 8, xcd = blk % 8;
+        blk = (xcd < r8_ ? xcd * (q8 + 1) : r8_ * (q8 + 1) + (xcd - r8_) * q8) + blk / 8;
+    }
+    const unsigned tiles = (unsigned)a.tiles;
     const unsigned b = blk / tiles, tile = blk % tiles;
     const int tid = threadIdx.x, g = tid % G, jt = tid / G;
     /* first passes (B == 1): G consecutive m; later passes (A == 1): G consecutive q */
@@ -240,6 +246,10 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     a.sgn = l->sgn;
     a.conj = l->conj;
     a.batch = l->batch;
+    {
+        const char *e = getenv("HSFFT_MR_XCD");
+        a.xcd = e ? atoi(e) : 1; /* c3: 78-80 -> 84-88 GSamples/s */
+    }
     const long long ext = v->first ? p->A : p->B;
     a.tiles = (int)((ext + v->G - 1) / v->G);
     a.tiles_q = v->first ? 1 : a.tiles;
