@@ -21,6 +21,24 @@ namespace bpf {
 
 using r8::Args;
 
+/* block -> (row group, 8-column tile).  Default: XCD-aware remap, row-group major (every XCD
+ * sweeps all 64 tiles).  a.tile_major: XCD x (blockIdx % 8 under round-robin dispatch; speed
+ * only, never correctness) owns tiles [8x, 8x+8) of every row group, so the per-tile tables
+ * (hk: 64 KiB per tile, the chirp) an XCD reads are 1/8 of them -- 512 KiB, L2-resident. */
+__device__ __forceinline__ void split_block(const Args &a, unsigned &bg, unsigned &tile)
+{
+    const unsigned tiles = (unsigned)a.tiles;
+    if (a.tile_major) {
+        const unsigned x = blockIdx.x % 8, r = blockIdx.x / 8, tpx = tiles / 8;
+        tile = x * tpx + r % tpx;
+        bg = r / tpx;
+    } else {
+        const unsigned blk = pf::xcd_remap(blockIdx.x);
+        bg = blk / tiles;
+        tile = blk % tiles;
+    }
+}
+
 /* hk product of the spectrum (ref :1803-1827 -- r8::store_hook HS_STORE_SPEC) */
 template <int DIR>
 __device__ __forceinline__ void spec(double &yr, double &yi, double2 k)
@@ -69,9 +87,8 @@ __global__ __launch_bounds__(512, 4) void k_bfirst(Args a)
     constexpr unsigned A = 512;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *ltw = lds + P * G; /* tw[0, 511): stages L = 8 (kloc < 8) and 64 */
-    const unsigned blk = pf::xcd_remap(blockIdx.x);
-    const unsigned tiles = (unsigned)a.tiles;
-    const unsigned bg = blk / tiles, tile = blk % tiles;
+    unsigned bg, tile;
+    split_block(a, bg, tile);
     const unsigned tid0 = threadIdx.x;
     const unsigned b0 = bg * T, nb = (unsigned)a.batch, nsig = (unsigned)a.nsig;
     const unsigned m0 = tile * G;
@@ -135,9 +152,8 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
     constexpr unsigned B = 512;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *ltw = lds + P * G; /* forward runs, 504 entries */
-    const unsigned blk = pf::xcd_remap(blockIdx.x);
-    const unsigned tiles = (unsigned)a.tiles;
-    const unsigned bg = blk / tiles, tile = blk % tiles;
+    unsigned bg, tile;
+    split_block(a, bg, tile);
     const unsigned tid0 = threadIdx.x, q0 = tile * G;
     const unsigned b0 = bg * T, nb = (unsigned)a.batch;
     const double2 *hk = a.saux;
@@ -207,9 +223,8 @@ __global__ __launch_bounds__(512, 4) void k_blast(Args a)
     constexpr unsigned B = 512;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *ltw = lds + P * G;
-    const unsigned blk = pf::xcd_remap(blockIdx.x);
-    const unsigned tiles = (unsigned)a.tiles;
-    const unsigned bg = blk / tiles, tile = blk % tiles;
+    unsigned bg, tile;
+    split_block(a, bg, tile);
     const unsigned tid0 = threadIdx.x, q0 = tile * G;
     const unsigned b0 = bg * T, nb = (unsigned)a.batch;
     const unsigned nsig = (unsigned)a.nsig;
@@ -331,6 +346,7 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     a.nsig = nsig;
     a.batch = batch;
     a.tiles = a.tiles_q = 512 / 8;
+    a.tile_major = env("HSFFT_BLUE_XT", 1) ? 1 : 0; /* c4 20.9 -> 21.4; tiles % 8 == 0: grid % 8 == 0 */
     const long long grid = a.tiles * ((batch + T - 1) / T);
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     /* image + twiddle runs (k_bfirst: 511; k_bmid: 504 forward runs + 511 inverse entries) */
