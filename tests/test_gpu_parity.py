@@ -303,6 +303,17 @@ def test_multi_device_api_single_gpu():
     assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), oracle_rows(x, 1))
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", list(range(12, 24)))
+def test_power_of_two_sweep_both_signs(k):
+    """every power of two 2^12 .. 2^23 (one- and two-pass plans: the pipelined / paired-load
+    kernels' applicability conditions on A, B, P), 3 rows, both signs, bit-exact vs oracle"""
+    n = 1 << k
+    batch = 3 if k <= 21 else 1
+    x = T.complex_input(n, 0x5EED ^ k, batch=batch).reshape(batch, n)
+    for sgn in (1, -1):
+        assert T.bits_equal(gpu_c2c_batched(n, sgn, x), oracle_rows(x, sgn)), (n, sgn)
+
+
 def test_two_pass_2pow21_batched():
     """2^21 = [8,8,8,8] (4096-point first pass) + [8,8,8]: bit-exact vs the oracle."""
     n = 1 << 21
