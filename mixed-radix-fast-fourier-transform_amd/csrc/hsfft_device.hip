@@ -783,12 +783,12 @@ int hsd_blue_first(const void *in, long long idist, void *out, long long odist, 
 }
 
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
-                 long long B, int batch, int sgn)
+                 long long B, int batch, int sgn, int compact)
 {
     const char *e = getenv("HSFFT_R2C_FUSE");
-    if (!(e && atoi(e) == 2)) { /* pf::k_r2c_fused (default), 2: the older r8::k_r2c_last */
-        const int rc = pf::launch_r2c_fused(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream());
-        if (rc <= 0) return rc;
+    if (compact || !(e && atoi(e) == 2)) { /* pf::k_r2c_fused (default), 2: the older r8::k_r2c_last */
+        const int rc = pf::launch_r2c_fused(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream(), compact != 0);
+        if (rc <= 0 || compact) return rc;
     }
     return r8::launch_r2c_last(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream());
 }

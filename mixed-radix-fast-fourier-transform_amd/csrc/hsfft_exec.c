@@ -724,7 +724,7 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
 }
 
 int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X, long long xdist, const void *tw2,
-                 int batch)
+                 int batch, int compact)
 {
     const hsd_pass *p0 = &e->pass[0], *p1 = &e->pass[1];
     if (e->lt != 0 || e->npass != 2 || p1->variant != HS_KV_R8X3 || p1->nst != 3 || p1->P != 512 || p1->A != 1 ||
@@ -734,7 +734,7 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
     if (!ds) return HSFFT_ERR_DEVICE;
     int rc = launch_pass(e, ds, 0, in, idist, Z, e->M, batch, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN,
                          NULL, e->M);
-    if (!rc && hsd_r2c_last(Z, e->M, X, xdist, ds->d_tw, tw2, e->M, p1->B, batch, e->sgn)) {
+    if (!rc && hsd_r2c_last(Z, e->M, X, xdist, ds->d_tw, tw2, e->M, p1->B, batch, e->sgn, compact)) {
         hs_seterr("r2c last pass: %s", hsd_errstr());
         rc = HSFFT_ERR_DEVICE;
     }

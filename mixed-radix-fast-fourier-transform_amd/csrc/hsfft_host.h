@@ -57,7 +57,7 @@ int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long lo
 /* r2c with the split fused into the last c2c pass: returns 1 when the plan's schedule does
  * not allow it (caller falls back to c2c + split), 0 on success, < 0 on error */
 int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X, long long xdist, const void *tw2,
-                 int batch);
+                 int batch, int compact);
 /* scratch buffers per device: class 0..2 chain pool, 3 Bluestein mid, 4 real staging, 5-7 misc,
  * 8 Bluestein second mid */
 void *hs_scratch(int cls, size_t bytes);

@@ -92,9 +92,10 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l);
 /* 1 if the register kernel has an instantiation for [r0, 8^n8] with this tile */
 int r8_has_variant(int r0, int n8, int G, int Wq, int first);
 int mr_has_variant(const hsd_pass *p);
-/* r2c: last c2c pass ([8,8,8], A == 1) + the real.c split in one kernel */
+/* r2c: last c2c pass ([8,8,8], A == 1) + the real.c split in one kernel; compact: rows of
+ * h+1 bins (hsfft_r2c_batched_compact) instead of the mirrored N */
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
-                 long long B, int batch, int sgn);
+                 long long B, int batch, int sgn, int compact);
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
 int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
                  int conj, int dir, int sgn2, int conj2); /* hsfft_pass_mr.h has a kernel for this pass */

@@ -395,7 +395,8 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
  * q-columns [8j+1, 8j+9) ("lo") and [B-8j-8, B-8j) ("hi") are closed under the pairing.  A
  * workgroup transforms both tiles (k_b512's stages: stage-0/1 twiddle runs in LDS, stage-2
  * twiddles coalesced and redistributed), swaps the hi tile through LDS and writes X[k],
- * X[N-k], X[h-k], X[h+k] of its lo tile.  Tile j == B/16 is column 0 (u <-> P-u, X[0], X[h]).
+ * X[N-k], X[h-k], X[h+k] of its lo tile (COMPACT: rows of h+1 bins, X[k] and X[h-k] only).
+ * Tile j == B/16 is column 0 (u <-> P-u, X[0], X[h]).
  * Saves the c2c output's write and re-read (16 of 56 bytes per real sample). */
 /* one tile's row loads, its stage-0/1 twiddle runs (-> ltw) and stage-2 twiddles (coalesced,
  * redistributed through the image: every earlier reader of the image must be done) */
@@ -446,7 +447,7 @@ __device__ __forceinline__ void r2c_stages(double (&xr)[8], double (&xi)[8], con
     stage<8, SGN>(xr, xi, w2, false);
 }
 
-template <int SGN>
+template <int SGN, bool COMPACT>
 __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -486,10 +487,10 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
             double re, im;
             r8::r2c_pair(zk, zh, w2t[k], re, im);
             X[k] = make_double2(re, im);
-            X[N - k] = make_double2(re, -im);
+            if (!COMPACT) X[N - k] = make_double2(re, -im);
             r8::r2c_pair(zh, zk, w2t[hk], re, im);
             X[hk] = make_double2(re, im);
-            X[N - hk] = make_double2(re, -im);
+            if (!COMPACT) X[N - hk] = make_double2(re, -im);
         }
     } else { /* column 0: k = u*B pairs with (P-u)*B */
         r2c_load(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
@@ -511,7 +512,7 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
                 double re, im;
                 r8::r2c_pair(zk, zh, w2t[k], re, im);
                 X[k] = make_double2(re, im);
-                X[N - k] = make_double2(re, -im);
+                if (!COMPACT) X[N - k] = make_double2(re, -im);
             }
         }
     }
@@ -519,7 +520,7 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
 
 /* returns 1 if not applicable, 0 on launch, < 0 on error */
 inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2,
-                            long long h, long long B, int batch, int sgn, hipStream_t st)
+                            long long h, long long B, int batch, int sgn, hipStream_t st, bool compact = false)
 {
     if (B % 16 || B * 512 != h || h > 0x40000000LL || (sgn != 1 && sgn != -1)) return 1;
     Args a;
@@ -537,7 +538,8 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     const long long grid = a.tiles * (long long)batch;
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     const size_t lds = (size_t)(512 * 8 + 504) * sizeof(double2);
-    void (*fn)(Args, unsigned) = sgn == 1 ? k_r2c_fused<1> : k_r2c_fused<-1>;
+    void (*fn)(Args, unsigned) = compact ? (sgn == 1 ? k_r2c_fused<1, true> : k_r2c_fused<-1, true>)
+                                         : (sgn == 1 ? k_r2c_fused<1, false> : k_r2c_fused<-1, false>);
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a, (unsigned)h);
     HCHK(hipGetLastError());

@@ -129,7 +129,7 @@ int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, 
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         /* x[2k], x[2k+1] packed as complex = the same bytes (ref real.c:99-103) */
-        rc = hs_r2c_fused(e, d_in + c0 * N, h, Z, d_out + c0 * N, N, tw2, cb);
+        rc = hs_r2c_fused(e, d_in + c0 * N, h, Z, d_out + c0 * N, N, tw2, cb, 0);
         if (rc == 1) {
             rc = hs_c2c_rows(e, d_in + c0 * N, h, Z, h, cb);
             if (!rc) rc = hsd_r2c_post(Z, tw2, d_out + c0 * N, h, cb, h, N) ? HSFFT_ERR_DEVICE : 0;
@@ -161,9 +161,12 @@ int hsfft_r2c_batched_compact(fft_real_object r, const fft_type *d_in, fft_data 
     if (!Z) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch && !rc; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
-        rc = hs_c2c_rows(e, d_in + c0 * N, h, Z, h, cb);
-        if (!rc)
-            rc = hsd_r2c_post_compact(Z, tw2, d_out + c0 * (h + 1), h, cb, h, h + 1) ? HSFFT_ERR_DEVICE : 0;
+        rc = hs_r2c_fused(e, d_in + c0 * N, h, Z, d_out + c0 * (h + 1), h + 1, tw2, cb, 1);
+        if (rc == 1) {
+            rc = hs_c2c_rows(e, d_in + c0 * N, h, Z, h, cb);
+            if (!rc)
+                rc = hsd_r2c_post_compact(Z, tw2, d_out + c0 * (h + 1), h, cb, h, h + 1) ? HSFFT_ERR_DEVICE : 0;
+        }
     }
     return rc;
 }

@@ -179,10 +179,12 @@ def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("n,batch", [(8, 3), (1000, 5), (1 << 16, 4), (1 << 22, 2), (2 * 99991, 2)])
-def test_r2c_compact_bit_exact(n, batch):
+@pytest.mark.parametrize("fuse", ["0", "1"])
+@pytest.mark.parametrize("n,batch", [(8, 3), (1000, 5), (1 << 16, 4), (1 << 19, 3), (1 << 22, 2), (2 * 99991, 2)])
+def test_r2c_compact_bit_exact(n, batch, fuse, monkeypatch):
     """hsfft_r2c_batched_compact: bins 0..N/2 per row, bit-identical to the reference-layout
-    output's first N/2+1 bins (and so to the oracle)"""
+    output's first N/2+1 bins (and so to the oracle); split fused into the last pass or not"""
+    monkeypatch.setenv("HSFFT_R2C_FUSE", fuse)
     x = T.real_input(n, 0xC0 ^ n, batch=batch).reshape(batch, n)
     rp = hsfft.RealPlan(n, 1)
     din = hsfft.DeviceBuffer.from_array(x)
