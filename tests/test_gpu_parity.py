@@ -190,16 +190,23 @@ def test_real_small_fixtures(golden):
             assert T.bits_equal(y, data[key]), key
 
 
-def test_c2r_batched_matches_oracle():
-    n = 1 << 16
-    X = T.oracle_r2c(T.real_input(n, 11, batch=3).reshape(3, n), 1)
+@pytest.mark.parametrize("n,rows", [(1 << 16, 3), (1 << 22, 2), (2 * 99991, 2), (12600, 5)])
+def test_c2r_batched_matches_oracle(n, rows):
+    """c2r (ref real.c:150-193) at scale: the inverse pre-twiddle kernel + the sgn=-1 c2c
+    (paired-load first pass and k_b512 at 2^22, Bluestein at 2*99991, mixed radix at 12600),
+    bit-exact; where the reference's transform is exact (no D2 twiddle quirk) the round trip
+    r2c -> c2r also returns N * x to 1e-12"""
+    x = T.real_input(n, 11, batch=rows).reshape(rows, n)
+    X = T.oracle_r2c(x, 1)
     rp = hsfft.RealPlan(n, -1)
     din = hsfft.DeviceBuffer.from_array(X)
-    dout = hsfft.DeviceBuffer(3 * n * 8)
-    hsfft.c2r_batched(rp, din, dout, 3)
-    y = dout.to_array(np.float64).reshape(3, n)
-    for b in range(3):
-        assert T.bits_equal(y[b], T.oracle_c2r(X[b], n, -1))
+    dout = hsfft.DeviceBuffer(rows * n * 8)
+    hsfft.c2r_batched(rp, din, dout, rows)
+    y = dout.to_array(np.float64).reshape(rows, n)
+    for b in range(rows):
+        assert T.bits_equal(y[b], T.oracle_c2r(X[b], n, -1)), b
+    if n != 12600:
+        assert np.max(np.abs(y / n - x)) < 1e-12
 
 
 def test_convolve_fixtures(golden):
