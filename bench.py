@@ -201,6 +201,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--r2c-compact", action="store_true",
                     help="c5 only: hsfft_r2c_batched_compact (N/2+1 bins per row) instead of the reference layout")
+    ap.add_argument("--c2r", action="store_true",
+                    help="c5 only: time hsfft_c2r_batched (the inverse real path, SURVEY.md §8f item 2) instead of r2c")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
     ap.add_argument("--dry-n", type=int, default=1024)
     ap.add_argument("--host-rows", type=int, default=0,
@@ -224,6 +226,8 @@ def main():
     kind, n, batch, seed, desc = cfg
     if args.r2c_compact and kind == "r2c":
         desc += " [compact N/2+1 output, hsfft_r2c_batched_compact]"
+    if args.c2r and kind == "r2c":
+        desc = desc.replace("r2c", "c2r", 1) + " [hsfft_c2r_batched, N/2+1 bins read per row]"
     if args.batch:
         batch = args.batch
     samples = n * batch
@@ -236,6 +240,22 @@ def main():
         run = lambda: hsfft.exec_batched(plan, din, dout, batch)  # noqa: E731
         bytes_per_sample = 32  # read 16 B + write 16 B
         dtype = "f64 (complex128)"
+    elif args.c2r:
+        plan = hsfft.RealPlan(n, -1)
+        # spectra in (N complex per row, bins 0..N/2 read), N reals out: the real output of all
+        # rows stays resident, the spectra are one chunk re-read per chunk of rows
+        chunk = min(batch, max(1, (64 << 30) // (n * 16)))
+        dout = hsfft.DeviceBuffer(samples * 8)
+        din = hsfft.DeviceBuffer(chunk * n * 16)
+        hsfft.fill_complex(din, chunk * n, seed, 0)
+
+        def run():
+            for c0 in range(0, batch, chunk):
+                cb = min(chunk, batch - c0)
+                hsfft.check(L.hsfft_c2r_batched(plan.ptr, ctypes.c_void_p(din.ptr),
+                                                ctypes.c_void_p(dout.ptr + c0 * n * 8), cb), "c2r_batched")
+        bytes_per_sample = 16  # read 8 B (N/2+1 bins) + write 8 B
+        dtype = "f64"
     else:
         plan = hsfft.RealPlan(n, 1)
         # the whole per-GPU input stays resident (4096 x 2^22 x 8 B = 128 GiB); the mirrored
@@ -279,7 +299,7 @@ def main():
         ev_ms, pms = hsfft.time_batched(plan, din, dout, batch, max(1, args.steps))
         npass = plan.num_passes()
         pass_ms = [p for p in pms[:npass] if p > 0]
-    elif args.r2c_compact:
+    elif args.r2c_compact or args.c2r:
         ev_ms = wall * 1e3
     else:
         ev_ms = hsfft.time_r2c_batched(plan, din, dout, chunk, max(1, args.steps)) * (batch / chunk)
@@ -338,7 +358,7 @@ def main():
                                 "pcie_gbs": round(2 * hx.nbytes / hs / 1e9, 1),
                                 "note": "host (pageable numpy) rows in and out, upload/transform/download overlapped; "
                                         "PCIe-inclusive, not the headline value"}
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.c2r:
         out["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:
         print(json.dumps(out), flush=True)
