@@ -191,6 +191,49 @@ def read_traffic(cfg_name, batch):
     return ent.get("hbm_bytes_per_launch")
 
 
+def bench_convolve(args, comm, ws, rank):
+    """batched linear convolution: r2c (compact, split fused) x2, spectral product on bins
+    0..P/2, c2r, scale, 'full' window copy -- the GPU form of convolve.c:74-214"""
+    L = hsfft.lib()
+    n = m = 1 << 20
+    rows = args.convolve
+    da = hsfft.DeviceBuffer(rows * n * 8)
+    db = hsfft.DeviceBuffer(rows * m * 8)
+    hsfft.fill_real(da, rows * n, 0x5EED0006, row_range(rank, rows)[0] * n)
+    hsfft.fill_real(db, rows * m, 0x5EED0007, row_range(rank, rows)[0] * m)
+    clen = n + m - 1
+    P = 1 << (clen - 1).bit_length()
+    dout = hsfft.DeviceBuffer(rows * clen * 8)
+
+    def run():
+        ln = L.hsfft_convolve_batched(b"full", b"linear", ctypes.c_void_p(da.ptr), n, ctypes.c_void_p(db.ptr), m,
+                                      ctypes.c_void_p(dout.ptr), rows)
+        if ln != clen:
+            raise SystemExit(f"convolve_batched returned {ln}: {L.hsfft_last_error()}")
+    for _ in range(args.warmup):
+        run()
+    hsfft.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    hsfft.synchronize()
+    comm.barrier()
+    wall = comm.max(time.perf_counter() - t0)
+    ms = wall / args.steps * 1e3
+    if rank == 0:
+        print(json.dumps({"metric": "GSamples/s (batched linear convolution, padded length P x rows per second)",
+                          "value": round(rows * P * ws / (ms / 1e3) / 1e9, 3), "unit": "GSamples/s", "n_gpus": ws,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                          "data": "synthetic (splitmix64 uniform [-1,1), generated in HBM)",
+                          "config": {"workload": f"convolve full/linear, {n} x {m} -> {clen} (P = {P}), {rows} rows",
+                                     "per_gpu_batch": rows, "global_batch": rows * ws,
+                                     "parallelism": f"batch-sharded x{ws} (no collective)"}}), flush=True)
+    for d in (da, db, dout):
+        d.free()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,6 +246,9 @@ def main():
                     help="c5 only: hsfft_r2c_batched_compact (N/2+1 bins per row) instead of the reference layout")
     ap.add_argument("--c2r", action="store_true",
                     help="c5 only: time hsfft_c2r_batched (the inverse real path, SURVEY.md §8f item 2) instead of r2c")
+    ap.add_argument("--convolve", type=int, default=0, metavar="ROWS",
+                    help="time hsfft_convolve_batched (SURVEY.md §8f item 1): ROWS linear 'full' convolutions "
+                         "of 2^20-sample pairs (P = 2^21); value = padded samples P x ROWS per second")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
     ap.add_argument("--dry-n", type=int, default=1024)
     ap.add_argument("--host-rows", type=int, default=0,
@@ -221,6 +267,10 @@ def main():
     if ndev < 1:
         raise SystemExit("bench.py: no GPU visible")
     hsfft.check(L.hsfft_set_device(local % ndev), "set_device")
+    if args.convolve:
+        bench_convolve(args, comm, ws, rank)
+        comm.close()
+        return
 
     cfg = CONFIGS[args.config]
     kind, n, batch, seed, desc = cfg

@@ -404,7 +404,7 @@ void hs_entry_release(const struct fft_set *obj)
 }
 
 /* ------------------------------------------------------------------ scratch */
-#define HS_NSCRATCH 10
+#define HS_NSCRATCH 11
 static void *g_scr[HS_MAX_DEV][HS_NSCRATCH];
 static size_t g_scr_sz[HS_MAX_DEV][HS_NSCRATCH];
 

@@ -59,7 +59,8 @@ int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long lo
 int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X, long long xdist, const void *tw2,
                  int batch, int compact);
 /* scratch buffers per device: class 0..2 chain pool, 3 Bluestein mid, 4 real staging, 5-7 misc,
- * 8 Bluestein second mid */
+ * 8 Bluestein second mid, 9 host pipeline, 10 convolution spectra */
+int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_type *d_out, int batch);
 void *hs_scratch(int cls, size_t bytes);
 
 #ifdef __cplusplus

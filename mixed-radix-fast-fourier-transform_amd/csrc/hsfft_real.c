@@ -180,6 +180,14 @@ int hsfft_c2r_batched(fft_real_object r, const fft_data *d_in, fft_type *d_out, 
     if (batch == 0) return 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    return hs_c2r_rows(r, d_in, 2LL * r->cobj->N, d_out, batch);
+}
+
+/* c2r of rows xdist complex apart (the reference layout: N; compact spectra: N/2+1 -- the
+ * pre-twiddle reads bins 0..N/2 only, ref real.c:169-179) */
+int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_type *d_out, int batch)
+{
+    int rc = 0;
     hs_entry *e = hs_entry_get(r->cobj);
     void *tw2 = tw2_device(r);
     if (!e || !tw2) return HSFFT_ERR_DEVICE;
@@ -190,7 +198,7 @@ int hsfft_c2r_batched(fft_real_object r, const fft_data *d_in, fft_type *d_out, 
     if (!Zi) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
-        rc = hsd_c2r_pre(d_in + c0 * N, tw2, Zi, h, cb, N, h) ? HSFFT_ERR_DEVICE : 0;
+        rc = hsd_c2r_pre(d_in + c0 * xdist, tw2, Zi, h, cb, xdist, h) ? HSFFT_ERR_DEVICE : 0;
         /* unpacking complex_output into interleaved reals is again a reinterpretation */
         if (!rc) rc = hs_c2c_rows(e, Zi, h, d_out + c0 * N, h, cb);
         if (rc) return rc;

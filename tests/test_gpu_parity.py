@@ -243,6 +243,29 @@ def test_convolve_batched_matches_oracle():
             assert T.bits_equal(y[r], o[:ln]), (typ, r)
 
 
+@pytest.mark.parametrize("n,m,typ", [(1 << 16, 1000, b"full"), (70000, 70000, b"same"), (5000, 300, b"valid")])
+def test_convolve_batched_at_scale(n, m, typ):
+    """hsfft_convolve_batched with P = 2^17 .. 2^18 (two-pass inner c2c, fused compact r2c
+    split, compact spectral product): every row bit-exact vs the oracle's convolve.c"""
+    L = hsfft.lib()
+    rows = 3
+    a = T.real_input(n, 15, batch=rows).reshape(rows, n)
+    b = T.real_input(m, 16, batch=rows).reshape(rows, m)
+    da, db = hsfft.DeviceBuffer.from_array(a), hsfft.DeviceBuffer.from_array(b)
+    dout = hsfft.DeviceBuffer(rows * (n + m) * 8)
+    ln = L.hsfft_convolve_batched(typ, b"linear", da.ptr, n, db.ptr, m, dout.ptr, rows)
+    assert ln > 0
+    y = dout.to_array(np.float64, rows * ln).reshape(rows, ln)
+    lib = T.oracle()
+    for r in range(rows):
+        o = np.zeros(2 * (n + m) + 8)
+        assert lib.orc_convolve(typ, b"linear", T.ptr(np.ascontiguousarray(a[r])), n,
+                                T.ptr(np.ascontiguousarray(b[r])), m, T.ptr(o), 0) == ln
+        assert T.bits_equal(y[r], o[:ln]), (typ, r)
+    for d in (da, db, dout):
+        d.free()
+
+
 def test_divergences_d3_d5_d6():
     """radix 13 (reference segfaults, D3), N=2^k+1 Bluestein (reference reads past its
     twiddles, D5), N=1 (reference exits, D6): correct results here, bit-exact vs oracle."""
