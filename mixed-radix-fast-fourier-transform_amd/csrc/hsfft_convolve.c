@@ -102,8 +102,8 @@ static int conv_setup(const char *conv_type, int n, int m, int *linear, int *cle
     return 0;
 }
 
-/* device core: a (rows of n), b (rows of m) -> res (rows of P, scaled) */
-static int conv_device(int P, const double *d_a, int n, const double *d_b, int m, double *d_res, int batch)
+/* device core: a (rows of n), b (rows of m) -> res (rows of P; divided by P if scale) */
+static int conv_device(int P, const double *d_a, int n, const double *d_b, int m, double *d_res, int batch, int scale)
 {
     fft_real_object f, iv;
     conv_plans(P, &f, &iv);
@@ -120,9 +120,8 @@ static int conv_device(int P, const double *d_a, int n, const double *d_b, int m
                  ? HSFFT_ERR_DEVICE : 0;
     if (!rc) rc = hsfft_r2c_batched_compact(f, pa, A, batch);
     if (!rc) rc = hsfft_r2c_batched_compact(f, pb, B, batch);
-    if (!rc) rc = hsd_cmul(A, B, A, cd, batch, cd) ? HSFFT_ERR_DEVICE : 0;
-    if (!rc) rc = hs_c2r_rows(iv, A, cd, d_res, batch);
-    if (!rc) rc = hsd_scale_real(d_res, P, batch, P, (double)P) ? HSFFT_ERR_DEVICE : 0;
+    if (!rc) rc = hs_c2r_product_rows(iv, A, B, cd, d_res, batch); /* product fused into the pre-twiddle */
+    if (!rc && scale) rc = hsd_scale_real(d_res, P, batch, P, (double)P) ? HSFFT_ERR_DEVICE : 0;
     if (!rc) rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
     return rc;
 }
@@ -149,7 +148,7 @@ int fft_convolve(const char *type, const char *conv_type, fft_type *input1, int 
     }
     double *d_b = d_a + length1;
     int rc = hsd_h2d(d_a, input1, sizeof(double) * (size_t)length1) || hsd_h2d(d_b, input2, sizeof(double) * (size_t)length2);
-    if (!rc) rc = conv_device(P, d_a, length1, d_b, length2, d_res, 1);
+    if (!rc) rc = conv_device(P, d_a, length1, d_b, length2, d_res, 1, 1);
     if (!rc && len > 0) rc = hsd_d2h(output, d_res + start, sizeof(double) * (size_t)len);
     hsfft_free(d_res);
     if (rc) {
@@ -172,8 +171,10 @@ int hsfft_convolve_batched(const char *type, const char *conv_type, const fft_ty
     if (rc) return rc;
     double *d_res = hsfft_malloc(sizeof(double) * (size_t)P * (size_t)batch);
     if (!d_res) return HSFFT_ERR_NOMEM;
-    rc = conv_device(P, d_a, length1, d_b, length2, d_res, batch);
-    if (!rc && len > 0) rc = hsd_copy_rows(d_res, P, start, len, d_out, len, len, batch) ? HSFFT_ERR_DEVICE : 0;
+    rc = conv_device(P, d_a, length1, d_b, length2, d_res, batch, 0);
+    /* the 1/P scale (convolve.c:157-160) fused into the window copy: same division per element */
+    if (!rc && len > 0)
+        rc = hsd_copy_rows_div(d_res, P, start, d_out, len, len, batch, (double)P) ? HSFFT_ERR_DEVICE : 0;
     if (!rc) rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
     hsfft_free(d_res);
     return rc ? rc : len;

@@ -342,6 +342,36 @@ __global__ void k_c2r_pre(const double2 *X, const double2 *w2, double2 *Zi, int 
     }
 }
 
+/* convolve.c:147-151's spectral product feeding real.c:169-179's inverse pre-twiddle in one
+ * pass: z[k] from (A.B)[k] and (A.B)[h-k]; each product is formed with k_cmul's expression
+ * (a pair's partner product is recomputed, same bits), so the c2r input is bit-identical */
+__device__ __forceinline__ double2 cmul1(double2 a, double2 c)
+{
+    return make_double2(a.x * c.x - a.y * c.y, a.x * c.y + a.y * c.x);
+}
+
+__global__ void k_c2r_pre_mul(const double2 *A, const double2 *Bv, const double2 *w2, double2 *Zi, int h,
+                              long long xdist, long long zdist)
+{
+    const int b = blockIdx.y;
+    const double2 *x = A + b * xdist, *y = Bv + b * xdist;
+    double2 *z = Zi + b * zdist;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < h; k += gridDim.x * blockDim.x) {
+        const double2 a = cmul1(x[k], y[k]), c = cmul1(x[h - k], y[h - k]), w = w2[k];
+        const double t1 = -a.y - c.y, t2 = -c.x + a.x;
+        z[k] = make_double2(a.x + c.x + (t1 * w.x) - (t2 * w.y), a.y - c.y + (t2 * w.x) + (t1 * w.y));
+    }
+}
+
+/* convolve.c:157-160 then :163-201: dst[b][i] = src[b][soff + i] / divisor, i < n */
+__global__ void k_copy_rows_div(const double *src, long long sdist, long long soff, double *dst, long long ddist,
+                                long long n, double divisor)
+{
+    const long long b = blockIdx.y;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        dst[b * ddist + i] = src[b * sdist + soff + i] / divisor;
+}
+
 /* ref convolve.c:147-151 */
 __global__ void k_cmul(const double2 *A, const double2 *Bv, double2 *C, long long n, long long dist)
 {
@@ -861,6 +891,26 @@ int hsd_scale_real(void *x, long long n, int batch, long long dist, double divis
 {
     if (batch > 65535) return -1;
     hipLaunchKernelGGL(k_scale_real, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (double *)x, n, dist, divisor);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_c2r_pre_mul(const void *A, const void *Bv, const void *tw2, void *Zin, int h, int batch, long long xdist,
+                    long long zdist)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_c2r_pre_mul, dim3(grid_for(h, 256), batch), dim3(256), 0, stream(), (const double2 *)A,
+                       (const double2 *)Bv, (const double2 *)tw2, (double2 *)Zin, h, xdist, zdist);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int hsd_copy_rows_div(const void *src, long long sdist, long long soff, void *dst, long long ddist, long long n,
+                      int batch, double divisor)
+{
+    if (batch > 65535) return -1;
+    hipLaunchKernelGGL(k_copy_rows_div, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (const double *)src,
+                       sdist, soff, (double *)dst, ddist, n, divisor);
     HCHK(hipGetLastError());
     return 0;
 }

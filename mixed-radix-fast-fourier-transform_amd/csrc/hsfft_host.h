@@ -61,6 +61,9 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
 /* scratch buffers per device: class 0..2 chain pool, 3 Bluestein mid, 4 real staging, 5-7 misc,
  * 8 Bluestein second mid, 9 host pipeline, 10 convolution spectra */
 int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_type *d_out, int batch);
+/* c2r of the product d_a .* d_b (compact or reference-layout rows xdist apart) */
+int hs_c2r_product_rows(fft_real_object r, const fft_data *d_a, const fft_data *d_b, long long xdist, fft_type *d_out,
+                        int batch);
 void *hs_scratch(int cls, size_t bytes);
 
 #ifdef __cplusplus

@@ -116,6 +116,11 @@ int hsd_r2c_post_compact(const void *Z, const void *tw2, void *X, int h, int bat
 int hsd_c2r_pre(const void *X, const void *tw2, void *Zin, int h, int batch, long long xdist, long long zdist);
 /* convolution helpers (convolve.c:147-160) */
 int hsd_cmul(const void *A, const void *Bv, void *C, long long n, int batch, long long dist);
+/* convolution: spectral product fused into the c2r pre-twiddle; scale fused into the window copy */
+int hsd_c2r_pre_mul(const void *A, const void *Bv, const void *tw2, void *Zin, int h, int batch, long long xdist,
+                    long long zdist);
+int hsd_copy_rows_div(const void *src, long long sdist, long long soff, void *dst, long long ddist, long long n,
+                      int batch, double divisor);
 int hsd_scale_real(void *x, long long n, int batch, long long dist, double divisor);
 int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
                   long long dlen, int batch);

@@ -183,6 +183,26 @@ int hsfft_c2r_batched(fft_real_object r, const fft_data *d_in, fft_type *d_out, 
     return hs_c2r_rows(r, d_in, 2LL * r->cobj->N, d_out, batch);
 }
 
+int hs_c2r_product_rows(fft_real_object r, const fft_data *d_a, const fft_data *d_b, long long xdist, fft_type *d_out,
+                        int batch)
+{
+    int rc = 0;
+    hs_entry *e = hs_entry_get(r->cobj);
+    void *tw2 = tw2_device(r);
+    if (!e || !tw2) return HSFFT_ERR_DEVICE;
+    const int h = r->cobj->N, N = 2 * h;
+    long long chunk = (long long)real_chunk_rows(h);
+    if (chunk > batch) chunk = batch;
+    fft_data *Zi = hs_scratch(4, sizeof(fft_data) * (size_t)(chunk * h));
+    if (!Zi) return HSFFT_ERR_NOMEM;
+    for (long long c0 = 0; c0 < batch && !rc; c0 += chunk) {
+        const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
+        rc = hsd_c2r_pre_mul(d_a + c0 * xdist, d_b + c0 * xdist, tw2, Zi, h, cb, xdist, h) ? HSFFT_ERR_DEVICE : 0;
+        if (!rc) rc = hs_c2c_rows(e, Zi, h, d_out + c0 * N, h, cb);
+    }
+    return rc;
+}
+
 /* c2r of rows xdist complex apart (the reference layout: N; compact spectra: N/2+1 -- the
  * pre-twiddle reads bins 0..N/2 only, ref real.c:169-179) */
 int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_type *d_out, int batch)
