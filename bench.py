@@ -279,6 +279,7 @@ def main():
     if args.c2r and kind == "r2c":
         desc = desc.replace("r2c", "c2r", 1) + " [hsfft_c2r_batched, N/2+1 bins read per row]"
     if args.batch:
+        desc += f" [per-GPU batch overridden to {args.batch}: not the BASELINE workload]"
         batch = args.batch
     samples = n * batch
     chunk = batch
