@@ -100,13 +100,26 @@ void free_real_fft(fft_real_object r)
     free(r);
 }
 
-static size_t real_chunk_rows(int h)
+/* row chunk for the inner c2c's intermediate Z (scratch class 4): HSFFT_CHUNK_MB of Z per
+ * chunk, default 16 GiB (measured, 4096 x 2^22 r2c, fused split: 2 GiB 91.7, 4 GiB 94.1,
+ * 8 GiB 98.3, 16 GiB 99.9 GSamples/s -- longer launches fill the chip better); halved while
+ * the allocation fails, so a device with less free HBM still runs, in smaller chunks */
+static fft_data *real_chunk(int h, int batch, long long *chunk)
 {
     const char *s = getenv("HSFFT_CHUNK_MB");
-    /* measured (4096 x 2^22 r2c): 256 MiB chunks under-fill pass B; 1 GiB 74, 4 GiB 78 GSamples/s */
-    size_t bytes = (size_t)(s ? atof(s) : 4096.0) * (1u << 20);
-    size_t rows = bytes / (sizeof(fft_data) * (size_t)h);
-    return rows ? rows : 1;
+    const size_t bytes = (size_t)(s ? atof(s) : 16384.0) * (1u << 20);
+    long long rows = (long long)(bytes / (sizeof(fft_data) * (size_t)h));
+    if (rows < 1) rows = 1;
+    if (rows > batch) rows = batch;
+    for (;;) {
+        fft_data *Z = hs_scratch(4, sizeof(fft_data) * (size_t)(rows * h));
+        if (Z || rows == 1) {
+            *chunk = rows;
+            if (!Z) hs_seterr("scratch allocation of %lld bytes failed", (long long)(rows * h * 16));
+            return Z;
+        }
+        rows = (rows + 1) / 2;
+    }
 }
 
 int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, int batch)
@@ -122,9 +135,8 @@ int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, 
     void *tw2 = tw2_device(r);
     if (!e || !tw2) return HSFFT_ERR_DEVICE;
     const int h = r->cobj->N, N = 2 * h;
-    long long chunk = (long long)real_chunk_rows(h);
-    if (chunk > batch) chunk = batch;
-    fft_data *Z = hs_scratch(4, sizeof(fft_data) * (size_t)(chunk * h));
+    long long chunk;
+    fft_data *Z = real_chunk(h, batch, &chunk);
     if (!Z) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
@@ -155,9 +167,8 @@ int hsfft_r2c_batched_compact(fft_real_object r, const fft_type *d_in, fft_data 
     void *tw2 = tw2_device(r);
     if (!e || !tw2) return HSFFT_ERR_DEVICE;
     const int h = r->cobj->N, N = 2 * h;
-    long long chunk = (long long)real_chunk_rows(h);
-    if (chunk > batch) chunk = batch;
-    fft_data *Z = hs_scratch(4, sizeof(fft_data) * (size_t)(chunk * h));
+    long long chunk;
+    fft_data *Z = real_chunk(h, batch, &chunk);
     if (!Z) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch && !rc; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
@@ -191,9 +202,8 @@ int hs_c2r_product_rows(fft_real_object r, const fft_data *d_a, const fft_data *
     void *tw2 = tw2_device(r);
     if (!e || !tw2) return HSFFT_ERR_DEVICE;
     const int h = r->cobj->N, N = 2 * h;
-    long long chunk = (long long)real_chunk_rows(h);
-    if (chunk > batch) chunk = batch;
-    fft_data *Zi = hs_scratch(4, sizeof(fft_data) * (size_t)(chunk * h));
+    long long chunk;
+    fft_data *Zi = real_chunk(h, batch, &chunk);
     if (!Zi) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch && !rc; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
@@ -212,9 +222,8 @@ int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_ty
     void *tw2 = tw2_device(r);
     if (!e || !tw2) return HSFFT_ERR_DEVICE;
     const int h = r->cobj->N, N = 2 * h;
-    long long chunk = (long long)real_chunk_rows(h);
-    if (chunk > batch) chunk = batch;
-    fft_data *Zi = hs_scratch(4, sizeof(fft_data) * (size_t)(chunk * h));
+    long long chunk;
+    fft_data *Zi = real_chunk(h, batch, &chunk);
     if (!Zi) return HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
