@@ -182,6 +182,28 @@ static int build_passes_pow2(hs_entry *e)
 static int build_passes(hs_entry *e)
 {
     if (build_passes_pow2(e) == 0) return 0;
+    if (e->nst <= HS_MAX_PASS_STAGES && env_int("HSFFT_MR_ROW", 1) && !env_int("HSFFT_GENERIC", 0)) {
+        /* a whole-row kernel for this radix list (hsfft_pass_mr.h k_row): one pass, one HBM
+         * round trip per row */
+        hsd_pass *p = &e->pass[0];
+        memset(p, 0, sizeof *p);
+        p->nst = e->nst;
+        p->P = 1;
+        for (int s = 0; s < e->nst; s++) {
+            p->radix[s] = e->stage_r[s];
+            p->gcs_off[s] = -1;
+            p->P *= e->stage_r[s];
+        }
+        p->leaf = e->first_leaf;
+        p->B = 1;
+        p->A = 1;
+        p->Wq = p->Wm = p->G = 1;
+        p->variant = HS_KV_MR;
+        if (p->P == e->M && mr_has_variant(p)) {
+            e->npass = 1;
+            return 0;
+        }
+    }
     const int pmax = pass_pmax();
     int s = 0, np = 0;
     long long B = 1;

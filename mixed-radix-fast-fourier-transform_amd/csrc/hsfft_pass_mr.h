@@ -182,34 +182,163 @@ __global__ __launch_bounds__(TPG * G) void k_pass(MArgs a)
     }
 }
 
+/* ------------------------------------------------------------------ whole-row kernel
+ * All six stages of a row in one launch (12600 = [3,3,5,5,7,8]: 197 KB per row, more than
+ * LDS but not more than a workgroup's registers): 1024 threads hold the row (<= 16 points
+ * each), the exchanges go through an image of P doubles -- real parts, then imaginary
+ * parts ("split", 98.4 KiB for 12600) -- and the row is read from and written to HBM once,
+ * instead of once per pass.  One workgroup per CU (LDS-bound); the other resident rows are
+ * simply the next workgroups.  Stage arithmetic is mr::stage's (same twiddles, operand
+ * order, k == 0 skips), so results are bit-identical to the two-pass schedule. */
+template <int R0, int R1, int R2, int R3, int R4, int R5>
+struct List6 {
+    static constexpr int R(int s)
+    {
+        return s == 0 ? R0 : s == 1 ? R1 : s == 2 ? R2 : s == 3 ? R3 : s == 4 ? R4 : R5;
+    }
+    static constexpr int P = R0 * R1 * R2 * R3 * R4 * R5;
+    static constexpr int Lloc(int s)
+    {
+        int l = 1;
+        for (int i = 0; i < s; i++) l *= R(i);
+        return l;
+    }
+    template <int TPG>
+    static constexpr int nmax()
+    {
+        int n = 0;
+        for (int i = 0; i < 6; i++) {
+            const int v = cdiv(P / R(i), TPG) * R(i);
+            n = v > n ? v : n;
+        }
+        return n;
+    }
+};
+
+/* exchange of one double per point (split image): stage (R, LLOC) outputs -> stage R2 inputs */
+template <int R, int LLOC, int R2, int P, int TPG>
+__device__ __forceinline__ void xchg1(double *x, double *ld, int jt)
+{
+    constexpr int NBF = P / R, NB = cdiv(NBF, TPG);
+    constexpr int L2 = LLOC * R, NBF2 = P / R2, NB2 = cdiv(NBF2, TPG), S2 = P / (L2 * R2);
+    __syncthreads(); /* the image's previous readers are done */
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        const int b = c * TPG + jt;
+        if (NB * TPG != NBF && b >= NBF) continue;
+        const int ml = b / LLOC, kloc = b % LLOC;
+#pragma unroll
+        for (int jj = 0; jj < R; jj++) ld[ml * LLOC * R + kloc + jj * LLOC] = x[c * R + jj];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NB2; c++) {
+        int b = c * TPG + jt;
+        if (NB2 * TPG != NBF2 && b >= NBF2) b = NBF2 - 1; /* idle slot: read something valid */
+        const int ml = b / L2, kloc = b % L2;
+#pragma unroll
+        for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[(ml + i * S2) * L2 + kloc];
+    }
+}
+
+template <int R, int LLOC, int R2, int P, int TPG>
+__device__ __forceinline__ void xchg_split(double *xr, double *xi, double *ld, int jt)
+{
+    xchg1<R, LLOC, R2, P, TPG>(xr, ld, jt);
+    xchg1<R, LLOC, R2, P, TPG>(xi, ld, jt);
+}
+
+template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG>
+__global__ __launch_bounds__(TPG) void k_row(MArgs a)
+{
+    using LS = List6<R0, R1, R2, R3, R4, R5>;
+    constexpr int P = LS::P;
+    constexpr int NM = LS::template nmax<TPG>();
+    extern __shared__ __attribute__((aligned(16))) double ldsd[];
+    const unsigned b = blockIdx.x;
+    const int jt = threadIdx.x;
+    const double2 *in = a.in + (long long)b * a.idist;
+    double2 *out = a.out + (long long)b * a.odist;
+    double xr[NM], xi[NM];
+    {
+        constexpr int NBF = P / R0, NB = cdiv(NBF, TPG);
+#pragma unroll
+        for (int c = 0; c < NB; c++) {
+            int bf = c * TPG + jt;
+            if (NB * TPG != NBF && bf >= NBF) bf = NBF - 1;
+#pragma unroll
+            for (int i = 0; i < R0; i++) {
+                const double2 v = in[bf + i * NBF];
+                xr[c * R0 + i] = v.x;
+                xi[c * R0 + i] = v.y;
+            }
+        }
+    }
+    stage<R0, 1, P, TPG, true>(xr, xi, a, jt, 0, true);
+    xchg_split<R0, 1, R1, P, TPG>(xr, xi, ldsd, jt);
+    stage<R1, LS::Lloc(1), P, TPG, false>(xr, xi, a, jt, 0, true);
+    xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, ldsd, jt);
+    stage<R2, LS::Lloc(2), P, TPG, false>(xr, xi, a, jt, 0, true);
+    xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, ldsd, jt);
+    stage<R3, LS::Lloc(3), P, TPG, false>(xr, xi, a, jt, 0, true);
+    xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, ldsd, jt);
+    stage<R4, LS::Lloc(4), P, TPG, false>(xr, xi, a, jt, 0, true);
+    xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, ldsd, jt);
+    stage<R5, LS::Lloc(5), P, TPG, false>(xr, xi, a, jt, 0, true);
+    /* last stage: butterfly kloc, outputs u = kloc + jj*LL */
+    constexpr int LL = LS::Lloc(5), NBFL = P / R5, NBL = cdiv(NBFL, TPG);
+#pragma unroll
+    for (int c = 0; c < NBL; c++) {
+        const int kloc = c * TPG + jt;
+        if (NBL * TPG != NBFL && kloc >= NBFL) continue;
+#pragma unroll
+        for (int jj = 0; jj < R5; jj++) out[kloc + jj * LL] = make_double2(xr[c * R5 + jj], xi[c * R5 + jj]);
+    }
+}
+
 typedef void (*kfn)(MArgs);
 
 struct Variant {
-    int nst, r[4], tpg, G;
+    int nst, r[6], tpg, G;
     bool first, leaf;
     kfn fn;
+    bool row; /* k_row: the whole row (A == B == 1) in one launch */
 };
 
-#define MRV(n, a, b, c, d, tpg, g, f, l) {n, {a, b, c, d}, tpg, g, f, l, k_pass<n, a, b, c, d, tpg, g, f, l>}
+#define MRV(n, a, b, c, d, tpg, g, f, l) {n, {a, b, c, d, 1, 1}, tpg, g, f, l, k_pass<n, a, b, c, d, tpg, g, f, l>, false}
 static const Variant k_variants[] = {
     /* 12600 = [3,3,5,5] + [7,8] (BASELINE config 3) */
     MRV(4, 3, 3, 5, 5, 45, 8, true, true),
     MRV(2, 7, 8, 1, 1, 8, 45, false, false),
     MRV(2, 7, 8, 1, 1, 8, 15, false, false),
     MRV(2, 7, 8, 1, 1, 8, 16, false, false),
+    /* 12600 whole-row (HSFFT_MR_ROW=0: the two passes above) */
+    {6, {3, 3, 5, 5, 7, 8}, 1024, 1, true, true, k_row<3, 3, 5, 5, 7, 8, 1024>, true},
 };
 #undef MRV
 
 /* picks a variant for a pass of the generic schedule; fills the tile geometry */
 inline const Variant *select(hsd_pass *p)
 {
+    if (p->nst == 6) { /* whole-row variants */
+        if (p->B != 1 || p->A != 1) return nullptr;
+        for (const Variant &v : k_variants) {
+            if (!v.row || v.leaf != (p->leaf != 0)) continue;
+            bool same = true;
+            for (int s = 0; s < 6; s++) same &= v.r[s] == p->radix[s];
+            if (!same) continue;
+            p->G = p->Wm = p->Wq = 1;
+            return &v;
+        }
+        return nullptr;
+    }
     if (p->nst < 1 || p->nst > 4) return nullptr;
     const bool first = p->B == 1;
     if (!first && p->A != 1) return nullptr;
     const Variant *best = nullptr;
     long long best_waste = -1;
     for (const Variant &v : k_variants) {
-        if (v.nst != p->nst || v.first != first || v.leaf != (p->leaf != 0)) continue;
+        if (v.row || v.nst != p->nst || v.first != first || v.leaf != (p->leaf != 0)) continue;
         bool same = true;
         for (int s = 0; s < p->nst; s++) same &= v.r[s] == p->radix[s];
         if (!same) continue;
@@ -249,6 +378,18 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     {
         const char *e = getenv("HSFFT_MR_XCD");
         a.xcd = e ? atoi(e) : 1; /* c3: 78-80 -> 84-88 GSamples/s */
+    }
+    if (v->row) {
+        const size_t lds = (size_t)p->P * sizeof(double);
+        if (l->batch <= 0 || lds > 160 * 1024) {
+            snprintf(g_err, sizeof g_err, "mr: bad row geometry batch=%d lds=%zu", l->batch, lds);
+            return -1;
+        }
+        a.tiles = a.tiles_q = 1;
+        HCHK(hipFuncSetAttribute((const void *)v->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(v->fn, dim3((unsigned)l->batch), dim3(v->tpg), lds, st, a);
+        HCHK(hipGetLastError());
+        return 0;
     }
     const long long ext = v->first ? p->A : p->B;
     a.tiles = (int)((ext + v->G - 1) / v->G);
