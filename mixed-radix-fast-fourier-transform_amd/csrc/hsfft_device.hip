@@ -447,8 +447,8 @@ int grid_for(long long n, int threads)
 }  // namespace
 
 #include "hsfft_pass_r8.h"
-#include "hsfft_pass_mr.h"
 #include "hsfft_pass_pf.h"
+#include "hsfft_pass_mr.h"
 #include "hsfft_fused.h"
 #include "hsfft_blue_pf.h"
 

@@ -296,6 +296,89 @@ __global__ __launch_bounds__(TPG) void k_row(MArgs a)
     }
 }
 
+/* k_row2: k_row walking rows (grid = one workgroup per CU), with the twiddles of the
+ * combine stages before the last ((R-1)*L entries at L-1: tw[0, Lloc(5)-1), 1574 for 12600,
+ * 24.6 KiB) copied to LDS once per workgroup, so only the last stage reads global (L2)
+ * twiddles; 32-bit index math; conjugation a template constant. */
+template <int R, int LLOC, int P, int TPG, bool LEAF, bool CONJ>
+__device__ __forceinline__ void rstage(double *xr, double *xi, const double2 *tws, int jt, int sgn)
+{
+    /* tws = tw + (LLOC - 1): stage twiddles tw[L-1 + (R-1)k + i-1] (ref :776-1561) */
+    constexpr int NBF = P / R, NB = cdiv(NBF, TPG);
+#pragma unroll
+    for (int c = 0; c < NB; c++) {
+        const int b = c * TPG + jt;
+        if (NB * TPG != NBF && b >= NBF) continue;
+        if constexpr (!LEAF) {
+            const unsigned k = (unsigned)b % (unsigned)LLOC;
+            const bool skip = (R == 4 || R == 5 || R == 7) && k == 0;
+            if (!skip) {
+                double2 t[R - 1];
+#pragma unroll
+                for (int i = 1; i < R; i++) t[i - 1] = tws[(R - 1) * k + i - 1];
+#pragma unroll
+                for (int i = 1; i < R; i++) hsb::twmul(xr[c * R + i], xi[c * R + i], t[i - 1].x, CONJ ? -t[i - 1].y : t[i - 1].y);
+            }
+        }
+        hsb::bfly<R>(&xr[c * R], &xi[c * R], sgn, LEAF);
+    }
+}
+
+template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ>
+__global__ __launch_bounds__(TPG) void k_row2(MArgs a)
+{
+    using LS = List6<R0, R1, R2, R3, R4, R5>;
+    constexpr int P = LS::P, NT = LS::Lloc(5) - 1; /* LDS twiddles tw[0, NT) */
+    constexpr int NM = LS::template nmax<TPG>();
+    extern __shared__ __attribute__((aligned(16))) double ldsd[];
+    double2 *ltw = reinterpret_cast<double2 *>(ldsd + P + (P & 1));
+    const int jt0 = threadIdx.x, sgn = a.sgn;
+    for (int i = jt0; i < NT; i += TPG) ltw[i] = a.tw[i];
+    /* (the first exchange's leading barrier orders these writes before any read) */
+#pragma unroll 1
+    for (unsigned b = blockIdx.x; b < (unsigned)a.batch; b += gridDim.x) {
+        int jt = jt0;
+        asm volatile("" : "+v"(jt)); /* keep per-row index math (and twiddle reads) in the loop */
+        const double2 *in = a.in + (long long)b * a.idist;
+        double2 *out = a.out + (long long)b * a.odist;
+        double xr[NM], xi[NM];
+        {
+            constexpr int NBF = P / R0, NB = cdiv(NBF, TPG);
+#pragma unroll
+            for (int c = 0; c < NB; c++) {
+                int bf = c * TPG + jt;
+                if (NB * TPG != NBF && bf >= NBF) bf = NBF - 1;
+#pragma unroll
+                for (int i = 0; i < R0; i++) {
+                    const double2 v = pf::ldg(in, (unsigned)(bf + i * NBF) * 16u);
+                    xr[c * R0 + i] = v.x;
+                    xi[c * R0 + i] = v.y;
+                }
+            }
+        }
+        rstage<R0, 1, P, TPG, true, CONJ>(xr, xi, ltw, jt, sgn);
+        xchg_split<R0, 1, R1, P, TPG>(xr, xi, ldsd, jt);
+        rstage<R1, LS::Lloc(1), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
+        xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, ldsd, jt);
+        rstage<R2, LS::Lloc(2), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
+        xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, ldsd, jt);
+        rstage<R3, LS::Lloc(3), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
+        xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, ldsd, jt);
+        rstage<R4, LS::Lloc(4), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(4) - 1), jt, sgn);
+        xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, ldsd, jt);
+        rstage<R5, LS::Lloc(5), P, TPG, false, CONJ>(xr, xi, a.tw + (LS::Lloc(5) - 1), jt, sgn);
+        constexpr int LL = LS::Lloc(5), NBFL = P / R5, NBL = cdiv(NBFL, TPG);
+#pragma unroll
+        for (int c = 0; c < NBL; c++) {
+            const int kloc = c * TPG + jt;
+            if (NBL * TPG != NBFL && kloc >= NBFL) continue;
+#pragma unroll
+            for (int jj = 0; jj < R5; jj++)
+                pf::stg(out, (unsigned)(kloc + jj * LL) * 16u, make_double2(xr[c * R5 + jj], xi[c * R5 + jj]));
+        }
+    }
+}
+
 typedef void (*kfn)(MArgs);
 
 struct Variant {
@@ -356,6 +439,12 @@ inline const Variant *select(hsd_pass *p)
     return best;
 }
 
+inline int env_row_v()
+{
+    const char *e = getenv("HSFFT_ROW_V");
+    return e ? atoi(e) : 2;
+}
+
 inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
 {
     hsd_pass tmp = *p;
@@ -378,6 +467,25 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     {
         const char *e = getenv("HSFFT_MR_XCD");
         a.xcd = e ? atoi(e) : 1; /* c3: 78-80 -> 84-88 GSamples/s */
+    }
+    if (v->row && env_row_v() == 2 && v->r[0] == 3 && v->r[1] == 3 && v->r[2] == 5 && v->r[3] == 5 && v->r[4] == 7 &&
+        v->r[5] == 8) {
+        constexpr int P = 12600, NT = 1574;
+        const size_t lds = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
+        if (l->batch <= 0) {
+            snprintf(g_err, sizeof g_err, "mr: bad row batch=%d", l->batch);
+            return -1;
+        }
+        kfn fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false>;
+        int ncu = 0, dev = 0;
+        HCHK(hipGetDevice(&dev));
+        HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        const int grid = l->batch < ncu ? l->batch : (ncu > 0 ? ncu : 256);
+        a.tiles = a.tiles_q = 1;
+        HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(1024), lds, st, a);
+        HCHK(hipGetLastError());
+        return 0;
     }
     if (v->row) {
         const size_t lds = (size_t)p->P * sizeof(double);
