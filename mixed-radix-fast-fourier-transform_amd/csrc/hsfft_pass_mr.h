@@ -324,12 +324,93 @@ __device__ __forceinline__ void rstage(double *xr, double *xi, const double2 *tw
     }
 }
 
-template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ>
+/* Stages 0 and 1 fused in registers (FUSE01): stage-1 butterfly (ml, kloc) reads output kloc
+ * of the stage-0 butterflies ml + S*i (S = P/(R0*R1), i < R1), so the R0*R1 points of group
+ * ml are closed under both stages -- a thread transforms whole groups and the first exchange
+ * disappears.  Same butterflies, twiddles and operand order as the unfused stages. */
+template <int R0, int R1, int P, int TPG, bool CONJ>
+__device__ __forceinline__ void fused01(double *xr, double *xi, const double2 *in, const double2 *ltw, double *ld,
+                                        int jt, int sgn)
+{
+    constexpr int S = P / (R0 * R1), NG = cdiv(S, TPG), NBF0 = P / R0, Q = R0 * R1;
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        int ml = g * TPG + jt;
+        if (NG * TPG != S && ml >= S) ml = S - 1; /* idle slot: compute on a valid group */
+        double *yr = xr + g * Q, *yi = xi + g * Q;
+        /* stage 0 (leaf): butterfly j1 of the group is b = ml + S*j1, inputs t = b + i*P/R0 */
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++)
+#pragma unroll
+            for (int i = 0; i < R0; i++) {
+                const double2 v = pf::ldg(in, (unsigned)(ml + S * j1 + i * NBF0) * 16u);
+                yr[j1 * R0 + i] = v.x;
+                yi[j1 * R0 + i] = v.y;
+            }
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++) hsb::bfly<R0>(&yr[j1 * R0], &yi[j1 * R0], sgn, true);
+        /* stage 1 (L = R0): butterfly kloc takes output kloc of stage-0 butterfly i */
+        double zr[Q], zi[Q];
+#pragma unroll
+        for (int kloc = 0; kloc < R0; kloc++) {
+#pragma unroll
+            for (int i = 0; i < R1; i++) {
+                zr[kloc * R1 + i] = yr[i * R0 + kloc];
+                zi[kloc * R1 + i] = yi[i * R0 + kloc];
+            }
+            const bool skip = (R1 == 4 || R1 == 5 || R1 == 7) && kloc == 0;
+            if (!skip) {
+#pragma unroll
+                for (int i = 1; i < R1; i++) {
+                    const double2 t = ltw[(R0 - 1) + (R1 - 1) * kloc + i - 1];
+                    hsb::twmul(zr[kloc * R1 + i], zi[kloc * R1 + i], t.x, CONJ ? -t.y : t.y);
+                }
+            }
+            hsb::bfly<R1>(&zr[kloc * R1], &zi[kloc * R1], sgn, false);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            yr[q] = zr[q];
+            yi[q] = zi[q];
+        }
+    }
+}
+
+/* exchange after fused01: output jj of stage-1 butterfly (ml, kloc) goes to ml*Q + kloc +
+ * jj*R0 (LLOC = R0), then stage R2's standard round-robin read (L2 = Q) */
+template <int R0, int R1, int R2, int P, int TPG>
+__device__ __forceinline__ void xchg1_f01(double *x, double *ld, int jt)
+{
+    constexpr int S = P / (R0 * R1), NG = cdiv(S, TPG), Q = R0 * R1;
+    constexpr int NBF2 = P / R2, NB2 = cdiv(NBF2, TPG), S2 = P / (Q * R2);
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        const int ml = g * TPG + jt;
+        if (NG * TPG != S && ml >= S) continue;
+#pragma unroll
+        for (int kloc = 0; kloc < R0; kloc++)
+#pragma unroll
+            for (int jj = 0; jj < R1; jj++) ld[ml * Q + kloc + jj * R0] = x[g * Q + kloc * R1 + jj];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NB2; c++) {
+        int b = c * TPG + jt;
+        if (NB2 * TPG != NBF2 && b >= NBF2) b = NBF2 - 1;
+        const int ml = b / Q, kloc = b % Q;
+#pragma unroll
+        for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[(ml + i * S2) * Q + kloc];
+    }
+}
+
+template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     using LS = List6<R0, R1, R2, R3, R4, R5>;
     constexpr int P = LS::P, NT = LS::Lloc(5) - 1; /* LDS twiddles tw[0, NT) */
-    constexpr int NM = LS::template nmax<TPG>();
+    constexpr int NM0 = LS::template nmax<TPG>(), NMF = cdiv(P / (R0 * R1), TPG) * R0 * R1;
+    constexpr int NM = F01 && NMF > NM0 ? NMF : NM0;
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
     double2 *ltw = reinterpret_cast<double2 *>(ldsd + P + (P & 1));
     const int jt0 = threadIdx.x, sgn = a.sgn;
@@ -342,24 +423,30 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         const double2 *in = a.in + (long long)b * a.idist;
         double2 *out = a.out + (long long)b * a.odist;
         double xr[NM], xi[NM];
-        {
-            constexpr int NBF = P / R0, NB = cdiv(NBF, TPG);
+        if constexpr (F01) {
+            fused01<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, ldsd, jt, sgn);
+            xchg1_f01<R0, R1, R2, P, TPG>(xr, ldsd, jt);
+            xchg1_f01<R0, R1, R2, P, TPG>(xi, ldsd, jt);
+        } else {
+            {
+                constexpr int NBF = P / R0, NB = cdiv(NBF, TPG);
 #pragma unroll
-            for (int c = 0; c < NB; c++) {
-                int bf = c * TPG + jt;
-                if (NB * TPG != NBF && bf >= NBF) bf = NBF - 1;
+                for (int c = 0; c < NB; c++) {
+                    int bf = c * TPG + jt;
+                    if (NB * TPG != NBF && bf >= NBF) bf = NBF - 1;
 #pragma unroll
-                for (int i = 0; i < R0; i++) {
-                    const double2 v = pf::ldg(in, (unsigned)(bf + i * NBF) * 16u);
-                    xr[c * R0 + i] = v.x;
-                    xi[c * R0 + i] = v.y;
+                    for (int i = 0; i < R0; i++) {
+                        const double2 v = pf::ldg(in, (unsigned)(bf + i * NBF) * 16u);
+                        xr[c * R0 + i] = v.x;
+                        xi[c * R0 + i] = v.y;
+                    }
                 }
             }
+            rstage<R0, 1, P, TPG, true, CONJ>(xr, xi, ltw, jt, sgn);
+            xchg_split<R0, 1, R1, P, TPG>(xr, xi, ldsd, jt);
+            rstage<R1, LS::Lloc(1), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
+            xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, ldsd, jt);
         }
-        rstage<R0, 1, P, TPG, true, CONJ>(xr, xi, ltw, jt, sgn);
-        xchg_split<R0, 1, R1, P, TPG>(xr, xi, ldsd, jt);
-        rstage<R1, LS::Lloc(1), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
-        xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, ldsd, jt);
         rstage<R2, LS::Lloc(2), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
         xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, ldsd, jt);
         rstage<R3, LS::Lloc(3), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
@@ -476,7 +563,10 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
             snprintf(g_err, sizeof g_err, "mr: bad row batch=%d", l->batch);
             return -1;
         }
-        kfn fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false>;
+        const char *ef = getenv("HSFFT_ROW_F01");
+        const bool f01 = ef ? atoi(ef) != 0 : true;
+        kfn fn = f01 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true>)
+                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, false> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, false>);
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));
         HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
