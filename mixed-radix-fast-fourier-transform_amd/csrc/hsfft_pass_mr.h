@@ -300,7 +300,7 @@ __global__ __launch_bounds__(TPG) void k_row(MArgs a)
  * combine stages before the last ((R-1)*L entries at L-1: tw[0, Lloc(5)-1), 1574 for 12600,
  * 24.6 KiB) copied to LDS once per workgroup, so only the last stage reads global (L2)
  * twiddles; 32-bit index math; conjugation a template constant. */
-template <int R, int LLOC, int P, int TPG, bool LEAF, bool CONJ>
+template <int R, int LLOC, int P, int TPG, bool LEAF, bool CONJ, bool TR = false>
 __device__ __forceinline__ void rstage(double *xr, double *xi, const double2 *tws, int jt, int sgn)
 {
     /* tws = tw + (LLOC - 1): stage twiddles tw[L-1 + (R-1)k + i-1] (ref :776-1561) */
@@ -315,7 +315,7 @@ __device__ __forceinline__ void rstage(double *xr, double *xi, const double2 *tw
             if (!skip) {
                 double2 t[R - 1];
 #pragma unroll
-                for (int i = 1; i < R; i++) t[i - 1] = tws[(R - 1) * k + i - 1];
+                for (int i = 1; i < R; i++) t[i - 1] = TR ? tws[(i - 1) * LLOC + k] : tws[(R - 1) * k + i - 1];
 #pragma unroll
                 for (int i = 1; i < R; i++) hsb::twmul(xr[c * R + i], xi[c * R + i], t[i - 1].x, CONJ ? -t[i - 1].y : t[i - 1].y);
             }
@@ -362,7 +362,7 @@ __device__ __forceinline__ void fused01(double *xr, double *xi, const double2 *i
             if (!skip) {
 #pragma unroll
                 for (int i = 1; i < R1; i++) {
-                    const double2 t = ltw[(R0 - 1) + (R1 - 1) * kloc + i - 1];
+                    const double2 t = ltw[(R0 - 1) + (i - 1) * R0 + kloc]; /* transposed (k_row2) */
                     hsb::twmul(zr[kloc * R1 + i], zi[kloc * R1 + i], t.x, CONJ ? -t.y : t.y);
                 }
             }
@@ -414,7 +414,24 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
     double2 *ltw = reinterpret_cast<double2 *>(ldsd + P + (P & 1));
     const int jt0 = threadIdx.x, sgn = a.sgn;
-    for (int i = jt0; i < NT; i += TPG) ltw[i] = a.tw[i];
+    /* LDS copy of the stage-1..4 twiddles, transposed within each stage's block [L-1, RL-1):
+     * entry (k, i) at L-1 + (i-1)*L + k, so the lanes of a wave (consecutive k) read
+     * consecutive 16-B words instead of words (R-1)*16 B apart (LDS bank conflicts) */
+    for (int e = LS::Lloc(1) - 1 + jt0; e < NT; e += TPG) { /* [0, R0-1): the leaf's, unused */
+        int L = LS::Lloc(1), R = R1;
+        if (e >= LS::Lloc(4) - 1) {
+            L = LS::Lloc(4);
+            R = R4;
+        } else if (e >= LS::Lloc(3) - 1) {
+            L = LS::Lloc(3);
+            R = R3;
+        } else if (e >= LS::Lloc(2) - 1) {
+            L = LS::Lloc(2);
+            R = R2;
+        }
+        const int loc = e - (L - 1), k = loc / (R - 1), i1 = loc % (R - 1);
+        ltw[L - 1 + i1 * L + k] = a.tw[e];
+    }
     /* (the first exchange's leading barrier orders these writes before any read) */
 #pragma unroll 1
     for (unsigned b = blockIdx.x; b < (unsigned)a.batch; b += gridDim.x) {
@@ -444,14 +461,14 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             }
             rstage<R0, 1, P, TPG, true, CONJ>(xr, xi, ltw, jt, sgn);
             xchg_split<R0, 1, R1, P, TPG>(xr, xi, ldsd, jt);
-            rstage<R1, LS::Lloc(1), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
+            rstage<R1, LS::Lloc(1), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
             xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, ldsd, jt);
         }
-        rstage<R2, LS::Lloc(2), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
+        rstage<R2, LS::Lloc(2), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
         xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, ldsd, jt);
-        rstage<R3, LS::Lloc(3), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
+        rstage<R3, LS::Lloc(3), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
         xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, ldsd, jt);
-        rstage<R4, LS::Lloc(4), P, TPG, false, CONJ>(xr, xi, ltw + (LS::Lloc(4) - 1), jt, sgn);
+        rstage<R4, LS::Lloc(4), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(4) - 1), jt, sgn);
         xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, ldsd, jt);
         rstage<R5, LS::Lloc(5), P, TPG, false, CONJ>(xr, xi, a.tw + (LS::Lloc(5) - 1), jt, sgn);
         constexpr int LL = LS::Lloc(5), NBFL = P / R5, NBL = cdiv(NBFL, TPG);
