@@ -373,6 +373,26 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
     assert T.bits_equal(y, T.oracle_r2c(x, sgn))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"}])
+@pytest.mark.parametrize("sgn", [1, -1])
+def test_12600_row_kernel_variants(env, sgn, monkeypatch):
+    """config 3's schedules, bit-exact vs the oracle, both signs, a batch that leaves the
+    row-walking grid uneven (300 rows over 256 workgroups): mr::k_row2 with stages 0-1 fused
+    (default) and unfused, mr::k_row (one workgroup per row), the two mixed-radix passes."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n, rows = 12600, 300
+    x = T.complex_input(n, 77, batch=rows).reshape(rows, n)
+    p = hsfft.Plan(n, sgn)
+    assert p.num_passes() == (2 if env.get("HSFFT_MR_ROW") == "0" else 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    hsfft.exec_batched(p, din, dout, rows)
+    y = dout.to_array(np.complex128).reshape(rows, n)
+    assert T.bits_equal(y, T.oracle_c2c(x, sgn))
+
+
 def _full_size_c2c(n, batch, seed, rows, sgn=1, tol=1e-13, roundtrip=True, flags=0):
     """a BASELINE config at its full per-GPU batch: sampled rows bit-exact vs the oracle and
     a forward/inverse round trip of the first rows (size-independent properties)."""

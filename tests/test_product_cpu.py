@@ -150,6 +150,22 @@ def test_pass_schedule_shapes():
         assert 1 <= p.num_passes() <= most, (n, p.num_passes())
 
 
+def test_12600_runs_as_one_whole_row_pass(monkeypatch):
+    """BASELINE config 3 (12600 = [3,3,5,5,7,8]) is scheduled as one whole-row pass
+    (mr::k_row2: one HBM round trip per row); HSFFT_MR_ROW=0 restores the two passes."""
+    assert hsfft.Plan(12600, 1).num_passes() == 1
+    assert hsfft.Plan(12600, -1).num_passes() == 1
+    code = textwrap.dedent(f"""
+        import sys; sys.path.insert(0, {T.PKG_DIR!r})
+        import hsfft
+        print(hsfft.Plan(12600, 1).num_passes())
+    """)
+    env = dict(os.environ, HSFFT_MR_ROW="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "2"
+
+
 @pytest.mark.skipif(os.environ.get("HIP_VISIBLE_DEVICES") is None and hsfft.device_count() > 0,
                     reason="a GPU is present")
 def test_compute_fails_loudly_without_gpu():
