@@ -6,8 +6,13 @@ already resident in HBM).  Multi-GPU: one process per GPU (torch.distributed.run
 transforms its own 4096 rows (weak scaling, no data-path collective -- the path shards by
 batch index); rank 0 prints one JSON line with the max-over-ranks time.
 
-Other configs for development: --config c3 (12600 x 65536), c4 (Bluestein 99991 x 8192),
-c5 (r2c 2^22 x 32768 over the job, chunked per GPU).
+Other configs: --config c1 (one N=1024 fft_exec on HOST buffers: latency, next to the
+reference timed in the same run), c3 (12600 x 65536), c4 (Bluestein 99991 x 8192), c5 (r2c
+2^22 x 32768 over the job, chunked per GPU).
+
+roofline: achieved = algorithmic bytes of the whole step (32 B per complex
+sample for c2c) / the event-timed step time, i.e. the transform as a whole, every launch of
+the step included; `pass_frac` lists the same figure per launch of a multi-launch step.
 """
 import argparse
 import ctypes
@@ -26,6 +31,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 CONFIGS = {
     # name: (kind, N, per-GPU batch, seed, description)
+    "c1": ("latency", 1024, 1, 0x5EED0001, "one N=1024 c2c forward fft_exec on host buffers (drop-in API)"),
     "c2": ("c2c", 1 << 20, 4096, 0x5EED0002, "batched c2c N=2^20, batch=4096 per GPU, fp64"),
     "c3": ("c2c", 12600, 65536, 0x5EED0003, "mixed-radix c2c N=12600, batch=65536 per GPU, fp64"),
     "c4": ("c2c", 99991, 8192, 0x5EED0004, "Bluestein c2c N=99991, batch=8192 per GPU, fp64"),
@@ -119,15 +125,52 @@ def dry_run(args, comm, ws, rank):
             "rank_checksums": checks}), flush=True)
 
 
+def host_cores():
+    """CPU cores this process may use: the affinity mask, capped by a cgroup CPU quota
+    (a GPU box shows the whole machine in os.cpu_count() but grants a share of it)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    use = min(aff, quota) if quota else aff
+    return max(1, use), {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "cpu_model": model}
+
+
 def cpu_baseline(cfg, seconds_target=15.0):
-    """The reference (oracle/_ref, compiled from the unmodified sources) timed on host cores
-    over a bounded sample: `sample` distinct transforms, swept `reps` times so that the timed
-    region is ~seconds_target of wall time.  Falls back to the oracle restatement ('port')
-    when the reference build is absent."""
+    """The reference (oracle/_ref, compiled from the unmodified sources) timed on ALL host
+    cores available to this process (one plan per thread) over a bounded sample: `sample`
+    distinct transforms, swept `reps` times so that the timed region is ~seconds_target of
+    wall time.  Falls back to the oracle restatement ('port') when the reference build is
+    absent."""
     kind, n, _, seed, _ = cfg
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, hostinfo = host_cores()
     ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
     sample = {("c2c", 1 << 20): 128, ("c2c", 12600): 8192, ("c2c", 99991): 64, ("r2c", 1 << 22): 32}.get((kind, n), 64)
+    sample = max(sample, threads)  # at least one transform per thread
     if os.path.exists(ref_so):
         L = ctypes.CDLL(ref_so)
         L.hsref_time_batch_reps.restype = ctypes.c_double
@@ -165,7 +208,7 @@ def cpu_baseline(cfg, seconds_target=15.0):
         src = "port"
     return {"value": round(n * sample * reps / secs / 1e9, 6), "unit": "GSamples/s", "cores": threads, "kind": src,
             "sample": f"{sample} distinct transforms of N={n} ({kind}) x {reps} sweeps, {threads} threads, "
-                      f"one plan per thread, {secs:.2f} s wall"}
+                      f"one plan per thread, {secs:.2f} s wall", **hostinfo}
 
 
 def traffic_entry(cfg_name):
@@ -177,18 +220,62 @@ def traffic_entry(cfg_name):
 
 
 def read_traffic(cfg_name, batch):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
-    FETCH_SIZE x2 [gfx950 calibration] + WRITE_SIZE, per MI355X_MICROARCH.md §HBM), valid only
-    for the batch it was measured at."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            ent = json.load(f).get(cfg_name)
-    except (OSError, ValueError):
-        return None
+    """HBM bytes of one whole step (every kernel of the step, per launch count) from the
+    committed PMC summary (rocprofv3 FETCH_SIZE x2 [gfx950 calibration] + WRITE_SIZE, per
+    MI355X_MICROARCH.md §HBM), valid only for the batch and schedule it was measured at."""
+    ent = traffic_entry(cfg_name)
     if not ent or ent.get("batch", CONFIGS[cfg_name][2]) != batch:
         return None
-    return ent.get("hbm_bytes_per_launch")
+    return ent.get("hbm_bytes_per_step")
+
+
+def bench_c1(args, comm, ws, rank):
+    """BASELINE config 1: ONE N=1024 forward c2c through the drop-in fft_exec on host buffers
+    (ref highSpeedFFT.c:1920; the reference takes ~9 us on one core).  Per-call latency is
+    timed call by call (ctypes overhead ~1 us included) and reported as the median; the
+    reference (oracle/_ref) is timed on one host core in the same run."""
+    import numpy as np
+    kind, n, _, seed, desc = CONFIGS["c1"]
+    plan = hsfft.Plan(n, 1)
+    dx = hsfft.DeviceBuffer(n * 16)
+    hsfft.fill_complex(dx, n, seed, 0)
+    x = dx.to_array(np.complex128, n)
+    y = np.zeros_like(x)
+    L = hsfft.lib()
+    px, py = x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p)
+    for _ in range(max(args.warmup, 20)):
+        L.fft_exec(plan.ptr, px, py)
+    iters = max(args.steps, 200)
+    lat = []
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        t = time.perf_counter()
+        L.fft_exec(plan.ptr, px, py)
+        lat.append(time.perf_counter() - t)
+    wall = comm.max(time.perf_counter() - t0)
+    lat.sort()
+    med_us = lat[len(lat) // 2] * 1e6
+    out = {"metric": "latency of one N=1024 c2c fft_exec on host buffers (BASELINE config 1)",
+           "value": round(med_us, 2), "unit": "us", "n_gpus": ws, "steps": iters, "warmup": max(args.warmup, 20),
+           "ms_per_step": round(wall / iters * 1e3, 5), "higher_is_better": False, "scaling": "replicas only",
+           "vs_baseline": None, "dtype": "f64 (complex128)", "data": "synthetic (splitmix64 uniform [-1,1))",
+           "config": {"workload": desc, "N": n, "per_gpu_batch": 1, "global_batch": ws,
+                      "parallelism": "replicas only"},
+           "latency_us": {"p10": round(lat[len(lat) // 10] * 1e6, 2), "median": round(med_us, 2),
+                          "p90": round(lat[len(lat) * 9 // 10] * 1e6, 2)}}
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
+    if rank == 0 and os.path.exists(ref_so) and not args.no_cpu_baseline:
+        R = ctypes.CDLL(ref_so)
+        R.hsref_time_batch_reps.restype = ctypes.c_double
+        R.hsref_time_batch_reps.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, ctypes.c_int]
+        reps = 200000
+        secs = R.hsref_time_batch_reps(n, 1, 0, 1, 1, seed, reps)
+        out["cpu_baseline"] = {"value": round(secs / reps * 1e6, 3), "unit": "us", "cores": 1, "kind": "reference",
+                               "sample": f"{reps} back-to-back fft_exec calls of N={n} on one core, {secs:.2f} s"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dx.free()
 
 
 def bench_convolve(args, comm, ws, rank):
@@ -250,6 +337,9 @@ def main():
                     help="time hsfft_convolve_batched (SURVEY.md §8f item 1): ROWS linear 'full' convolutions "
                          "of 2^20-sample pairs (P = 2^21); value = padded samples P x ROWS per second")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
+    ap.add_argument("--dump-rows", default="",
+                    help="c2c only: after the timed steps, save the first and last output row of this rank's "
+                         "shard with their global row indices to DIR/rank<r>.npz (multi-rank parity test)")
     ap.add_argument("--dry-n", type=int, default=1024)
     ap.add_argument("--host-rows", type=int, default=0,
                     help="also time hsfft_exec_batched_host on this many HOST-resident rows (PCIe-inclusive "
@@ -269,6 +359,10 @@ def main():
     hsfft.check(L.hsfft_set_device(local % ndev), "set_device")
     if args.convolve:
         bench_convolve(args, comm, ws, rank)
+        comm.close()
+        return
+    if args.config == "c1":
+        bench_c1(args, comm, ws, rank)
         comm.close()
         return
 
@@ -378,20 +472,20 @@ def main():
         "achieved_hbm_gbs": round(samples * bytes_per_sample * ws / (ms_per_step / 1e3) / 1e9, 1),
         "event_ms_per_step": round(ev_step_ms, 4),
     }
+    # the transform as a whole: algorithmic bytes of the step / event-timed step time
+    ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
+    ent = traffic_entry(args.config)
+    kern = ent.get("kernel", "").replace("void ", "") if ent.get("batch") == batch else ""
+    out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
+                       "algorithmic_bytes": samples * bytes_per_sample,
+                       "basis": f"whole step: {bytes_per_sample} B x N x batch / event-timed step time, all "
+                                f"{max(npass, 1)} launch(es) of the step",
+                       "kernel": kern or f"{max(npass, 1)} launch(es) per step"}
     if pass_ms:
-        dom = max(range(len(pass_ms)), key=lambda i: pass_ms[i])
-        ach = samples * bytes_per_sample / (pass_ms[dom] / 1e3) / 1e9
-        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
-                           "kernel": f"pass {dom} of {npass}", "pass_ms": [round(p, 4) for p in pass_ms]}
-        ent = traffic_entry(args.config)
-        if dom == 0 and ent.get("kernel"):
-            out["roofline"]["kernel"] += f" ({ent['kernel'].replace('void ', '')})"
-    else:
-        ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
-        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
-                           "kernel": "whole step (event timed)"}
+        out["roofline"]["pass_ms"] = [round(p, 4) for p in pass_ms]
+        out["roofline"]["pass_frac"] = [round(samples * bytes_per_sample / (p / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                                        for p in pass_ms]
     # practical HBM ceiling on this device: a 16-B-per-lane stream copy of the same buffers
     nbytes = min(din.nbytes, dout.nbytes) // 16 * 16
     cms = hsfft.bench_copy(din, dout, nbytes, 5)
@@ -409,6 +503,14 @@ def main():
                                 "pcie_gbs": round(2 * hx.nbytes / hs / 1e9, 1),
                                 "note": "host (pageable numpy) rows in and out, upload/transform/download overlapped; "
                                         "PCIe-inclusive, not the headline value"}
+    if args.dump_rows and kind == "c2c":
+        import numpy as np
+        g0 = row_range(rank, batch)[0]
+        picks = sorted({0, batch - 1})
+        rows = np.stack([dout.to_array(np.complex128, n, r * n * 16) for r in picks])
+        os.makedirs(args.dump_rows, exist_ok=True)
+        np.savez(os.path.join(args.dump_rows, f"rank{rank}.npz"), rows=rows,
+                 global_rows=np.array([g0 + r for r in picks]), n=n, seed=seed, world=ws)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.c2r:
         out["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:

@@ -37,6 +37,12 @@ int hsfft_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes);  /* synchron
 int hsfft_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes);  /* synchronous */
 int hsfft_memset(void *d_ptr, int value, size_t bytes);
 int hsfft_synchronize(void);
+/* Frees the library's scratch pool on the current device (intermediates, staging slots,
+ * convolution buffers) after waiting for queued work; the pool regrows on demand.  The pool
+ * otherwise persists for the process: up to the largest chunk a call needed (c2c chains
+ * HSFFT_CHUNK_MB, default 256 MiB x 2; Bluestein HSFFT_BLUE_CHUNK_MB, 4 GiB x 2; real paths
+ * HSFFT_REAL_CHUNK_MB, 16 GiB -- each halved while allocation fails). */
+int hsfft_release_scratch(void);
 void *hsfft_get_stream(void);            /* hipStream_t of the current device */
 const char *hsfft_last_error(void);
 
@@ -91,6 +97,13 @@ int hsfft_time_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *
 /* Stream-copy reference: `iters` device copies of `bytes` (multiple of 16) from d_src to
  * d_dst, event-timed; the practical HBM ceiling reported next to the FFT numbers. */
 int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms);
+
+/* --- threading -------------------------------------------------------------------------
+ * Every entry point is safe to call from several host threads at once, on shared or
+ * distinct plans (the reference's mixed-radix fft_exec is reentrant, highSpeedFFT.c:1920).
+ * Calls that run on the same device are serialised per call by a device lock (they share
+ * the device's stream and scratch pool); calls on different devices run concurrently.
+ * Freeing a plan while another thread still executes it remains a caller error. */
 
 /* --- multi-device (single process; one host thread per device, no collective) --------- */
 /* Shards the batch contiguously over devices 0..ndev-1: h-side arrays of per-device

@@ -32,36 +32,73 @@ int find_optimal_fft_length(int min_length, const char *conv_type, int length1, 
     exit(EXIT_FAILURE);
 }
 
+/* Plan cache: entries are reference counted -- a slot in use by any thread is never
+ * evicted; when every slot is busy the call builds a private pair and frees it afterwards. */
 #define HS_CONV_CACHE 8
 static pthread_mutex_t g_clock = PTHREAD_MUTEX_INITIALIZER;
 static struct {
-    int P, mode;
+    int P, mode, refs;
+    unsigned long long used; /* LRU stamp */
     fft_real_object f, i;
 } g_cache[HS_CONV_CACHE];
-static int g_cache_next;
+static unsigned long long g_cache_clock;
 
-static void conv_plans(int P, fft_real_object *f, fft_real_object *i)
+typedef struct {
+    fft_real_object f, i;
+    int slot; /* cache slot held, or -1 for a private pair */
+} conv_pair;
+
+static conv_pair conv_plans(int P)
 {
     const int mode = hsfft_get_twiddle_mode();
+    conv_pair cp = {NULL, NULL, -1};
     pthread_mutex_lock(&g_clock);
-    for (int k = 0; k < HS_CONV_CACHE; k++)
+    int victim = -1;
+    for (int k = 0; k < HS_CONV_CACHE; k++) {
         if (g_cache[k].f && g_cache[k].P == P && g_cache[k].mode == mode) {
-            *f = g_cache[k].f;
-            *i = g_cache[k].i;
+            g_cache[k].refs++;
+            g_cache[k].used = ++g_cache_clock;
+            cp.f = g_cache[k].f;
+            cp.i = g_cache[k].i;
+            cp.slot = k;
             pthread_mutex_unlock(&g_clock);
-            return;
+            return cp;
         }
-    const int slot = g_cache_next++ % HS_CONV_CACHE;
-    if (g_cache[slot].f) {
-        free_real_fft(g_cache[slot].f);
-        free_real_fft(g_cache[slot].i);
+        if (g_cache[k].refs == 0 && (victim < 0 || !g_cache[k].f || (g_cache[victim].f && g_cache[k].used < g_cache[victim].used)))
+            victim = k;
     }
-    g_cache[slot].P = P;
-    g_cache[slot].mode = mode;
-    g_cache[slot].f = fft_real_init(P, 1);
-    g_cache[slot].i = fft_real_init(P, -1);
-    *f = g_cache[slot].f;
-    *i = g_cache[slot].i;
+    if (victim >= 0) { /* evict the least recently used idle slot */
+        if (g_cache[victim].f) {
+            free_real_fft(g_cache[victim].f);
+            free_real_fft(g_cache[victim].i);
+        }
+        g_cache[victim].P = P;
+        g_cache[victim].mode = mode;
+        g_cache[victim].refs = 1;
+        g_cache[victim].used = ++g_cache_clock;
+        g_cache[victim].f = fft_real_init(P, 1);
+        g_cache[victim].i = fft_real_init(P, -1);
+        cp.f = g_cache[victim].f;
+        cp.i = g_cache[victim].i;
+        cp.slot = victim;
+        pthread_mutex_unlock(&g_clock);
+        return cp;
+    }
+    pthread_mutex_unlock(&g_clock);
+    cp.f = fft_real_init(P, 1);
+    cp.i = fft_real_init(P, -1);
+    return cp;
+}
+
+static void conv_plans_done(conv_pair cp)
+{
+    if (cp.slot < 0) {
+        free_real_fft(cp.f);
+        free_real_fft(cp.i);
+        return;
+    }
+    pthread_mutex_lock(&g_clock);
+    g_cache[cp.slot].refs--;
     pthread_mutex_unlock(&g_clock);
 }
 
@@ -105,15 +142,19 @@ static int conv_setup(const char *conv_type, int n, int m, int *linear, int *cle
 /* device core: a (rows of n), b (rows of m) -> res (rows of P; divided by P if scale) */
 static int conv_device(int P, const double *d_a, int n, const double *d_b, int m, double *d_res, int batch, int scale)
 {
-    fft_real_object f, iv;
-    conv_plans(P, &f, &iv);
+    const conv_pair cp = conv_plans(P);
+    fft_real_object f = cp.f, iv = cp.i;
     /* the reference multiplies all P mirrored bins (convolve.c:147-151), but its c2r reads
      * bins 0..P/2 only (real.c:169-179): compact spectra of P/2+1 bins give the same bits
      * with a third less traffic */
     const long long cd = P / 2 + 1;
     double *pa = hs_scratch(7, sizeof(double) * (size_t)P * 2 * (size_t)batch);
     fft_data *spec = hs_scratch(10, sizeof(fft_data) * (size_t)cd * 2 * (size_t)batch);
-    if (!pa || !spec) return HSFFT_ERR_NOMEM;
+    if (!pa || !spec) {
+        conv_plans_done(cp);
+        hs_seterr("convolution scratch allocation failed (%d rows of P = %d)", batch, P);
+        return HSFFT_ERR_NOMEM;
+    }
     double *pb = pa + (size_t)P * batch;
     fft_data *A = spec, *B = spec + (size_t)cd * batch;
     int rc = hsd_copy_rows(d_a, n, 0, n, pa, P, P, batch) || hsd_copy_rows(d_b, m, 0, m, pb, P, P, batch)
@@ -123,11 +164,12 @@ static int conv_device(int P, const double *d_a, int n, const double *d_b, int m
     if (!rc) rc = hs_c2r_product_rows(iv, A, B, cd, d_res, batch); /* product fused into the pre-twiddle */
     if (!rc && scale) rc = hsd_scale_real(d_res, P, batch, P, (double)P) ? HSFFT_ERR_DEVICE : 0;
     if (!rc) rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
+    conv_plans_done(cp);
     return rc;
 }
 
-int fft_convolve(const char *type, const char *conv_type, fft_type *input1, int length1, fft_type *input2,
-                 int length2, fft_type *output)
+static int convolve_locked(const char *type, const char *conv_type, fft_type *input1, int length1,
+                           fft_type *input2, int length2, fft_type *output)
 {
     if (input1 == NULL || input2 == NULL || output == NULL || length1 <= 0 || length2 <= 0) {
         fprintf(stderr, "Error: Invalid inputs for fft_convolve\n");
@@ -158,6 +200,15 @@ int fft_convolve(const char *type, const char *conv_type, fft_type *input1, int 
     return len;
 }
 
+int fft_convolve(const char *type, const char *conv_type, fft_type *input1, int length1, fft_type *input2,
+                 int length2, fft_type *output)
+{
+    const int d = hs_lock_device();
+    const int rc = convolve_locked(type, conv_type, input1, length1, input2, length2, output);
+    hs_unlock_device(d);
+    return rc;
+}
+
 int hsfft_convolve_batched(const char *type, const char *conv_type, const fft_type *d_a, int length1,
                            const fft_type *d_b, int length2, fft_type *d_out, int batch)
 {
@@ -169,13 +220,18 @@ int hsfft_convolve_batched(const char *type, const char *conv_type, const fft_ty
     if (batch == 0) return len;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    const int d = hs_lock_device();
     double *d_res = hsfft_malloc(sizeof(double) * (size_t)P * (size_t)batch);
-    if (!d_res) return HSFFT_ERR_NOMEM;
+    if (!d_res) {
+        hs_unlock_device(d);
+        return HSFFT_ERR_NOMEM;
+    }
     rc = conv_device(P, d_a, length1, d_b, length2, d_res, batch, 0);
     /* the 1/P scale (convolve.c:157-160) fused into the window copy: same division per element */
     if (!rc && len > 0)
         rc = hsd_copy_rows_div(d_res, P, start, d_out, len, len, batch, (double)P) ? HSFFT_ERR_DEVICE : 0;
     if (!rc) rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
     hsfft_free(d_res);
+    hs_unlock_device(d);
     return rc ? rc : len;
 }

@@ -19,14 +19,34 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "hsfft_butterfly.h"
 #include "hsfft_internal.h"
 
 namespace {
 
 thread_local char g_err[512];
+
+/* Lazily created per-device objects (streams, events): created once under g_init_mtx,
+ * published through the atomic flags, so host threads may race on first use. */
+std::mutex g_init_mtx;
+
+hipStream_t lazy_stream(hipStream_t (&tab)[HS_MAX_DEV], std::atomic<bool> (&ready)[HS_MAX_DEV], int dev)
+{
+    if (!ready[dev].load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> g(g_init_mtx);
+        if (!ready[dev].load(std::memory_order_relaxed)) {
+            if (hipStreamCreateWithFlags(&tab[dev], hipStreamNonBlocking) != hipSuccess) tab[dev] = 0;
+            ready[dev].store(true, std::memory_order_release);
+        }
+    }
+    return tab[dev];
+}
+
 hipStream_t g_stream[HS_MAX_DEV];
-bool g_stream_init[HS_MAX_DEV];
+std::atomic<bool> g_stream_init[HS_MAX_DEV];
 
 int set_err(hipError_t e, const char *what)
 {
@@ -41,44 +61,33 @@ int set_err(hipError_t e, const char *what)
     } while (0)
 
 hipStream_t g_stream2[HS_MAX_DEV], g_stream3[HS_MAX_DEV];
-bool g_stream2_init[HS_MAX_DEV], g_stream3_init[HS_MAX_DEV];
+std::atomic<bool> g_stream2_init[HS_MAX_DEV], g_stream3_init[HS_MAX_DEV];
 thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream */
 
-hipStream_t primary()
+int cur_dev()
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) dev = 0;
-    if (!g_stream_init[dev]) {
-        if (hipStreamCreateWithFlags(&g_stream[dev], hipStreamNonBlocking) != hipSuccess) g_stream[dev] = 0;
-        g_stream_init[dev] = true;
-    }
-    return g_stream[dev];
+    return dev;
 }
+
+hipStream_t primary() { return lazy_stream(g_stream, g_stream_init, cur_dev()); }
 
 /* the stream kernels are launched on: the library stream, or (inside a pipelined chain)
  * the second stream that runs pass B of chunk c while pass A of chunk c+1 runs */
 hipStream_t stream()
 {
     if (t_sidx == 0) return primary();
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) dev = 0;
-    if (t_sidx == 2) {
-        if (!g_stream3_init[dev]) {
-            if (hipStreamCreateWithFlags(&g_stream3[dev], hipStreamNonBlocking) != hipSuccess) g_stream3[dev] = 0;
-            g_stream3_init[dev] = true;
-        }
-        return g_stream3[dev];
-    }
-    if (!g_stream2_init[dev]) {
-        if (hipStreamCreateWithFlags(&g_stream2[dev], hipStreamNonBlocking) != hipSuccess) g_stream2[dev] = 0;
-        g_stream2_init[dev] = true;
-    }
-    return g_stream2[dev];
+    const int dev = cur_dev();
+    if (t_sidx == 2) return lazy_stream(g_stream3, g_stream3_init, dev);
+    return lazy_stream(g_stream2, g_stream2_init, dev);
 }
 
+/* event ring (cross-stream ordering) and timing events, per device; used under the
+ * device's API lock (hsfft_exec.c), created lazily under g_init_mtx */
 #define HS_NEV 64
 hipEvent_t g_ev[HS_MAX_DEV][HS_NEV];
-bool g_ev_init[HS_MAX_DEV];
+std::atomic<bool> g_ev_init[HS_MAX_DEV];
 
 /* ------------------------------------------------------------------ generic pass kernel */
 struct KArgs {
@@ -431,10 +440,22 @@ __global__ __launch_bounds__(256) void k_copyU(const v2d *__restrict__ a, v2d *_
     }
 }
 
-hipEvent_t g_t0, g_t1;
-bool g_timer_init = false;
-hipEvent_t g_pev[2 * HS_MAX_PASSES];
-bool g_pev_init = false;
+hipEvent_t g_t0[HS_MAX_DEV], g_t1[HS_MAX_DEV];
+hipEvent_t g_pev[HS_MAX_DEV][2 * HS_MAX_PASSES];
+std::atomic<bool> g_timer_init[HS_MAX_DEV];
+
+/* creates the per-device timing events once; false on failure */
+bool timer_events(int dev)
+{
+    if (g_timer_init[dev].load(std::memory_order_acquire)) return true;
+    std::lock_guard<std::mutex> g(g_init_mtx);
+    if (g_timer_init[dev].load(std::memory_order_relaxed)) return true;
+    if (hipEventCreate(&g_t0[dev]) != hipSuccess || hipEventCreate(&g_t1[dev]) != hipSuccess) return false;
+    for (int k = 0; k < 2 * HS_MAX_PASSES; k++)
+        if (hipEventCreate(&g_pev[dev][k]) != hipSuccess) return false;
+    g_timer_init[dev].store(true, std::memory_order_release);
+    return true;
+}
 
 int grid_for(long long n, int threads)
 {
@@ -699,9 +720,12 @@ int hsd_event_record(int i)
 {
     int dev = hsd_get_device();
     if (dev < 0 || dev >= HS_MAX_DEV) return -1;
-    if (!g_ev_init[dev]) {
-        for (int k = 0; k < HS_NEV; k++) HCHK(hipEventCreateWithFlags(&g_ev[dev][k], hipEventDisableTiming));
-        g_ev_init[dev] = true;
+    if (!g_ev_init[dev].load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> g(g_init_mtx);
+        if (!g_ev_init[dev].load(std::memory_order_relaxed)) {
+            for (int k = 0; k < HS_NEV; k++) HCHK(hipEventCreateWithFlags(&g_ev[dev][k], hipEventDisableTiming));
+            g_ev_init[dev].store(true, std::memory_order_release);
+        }
     }
     HCHK(hipEventRecord(g_ev[dev][i % HS_NEV], stream()));
     return 0;
@@ -710,7 +734,7 @@ int hsd_event_record(int i)
 int hsd_event_wait(int i)
 {
     int dev = hsd_get_device();
-    if (dev < 0 || dev >= HS_MAX_DEV || !g_ev_init[dev]) return -1;
+    if (dev < 0 || dev >= HS_MAX_DEV || !g_ev_init[dev].load(std::memory_order_acquire)) return -1;
     HCHK(hipStreamWaitEvent(stream(), g_ev[dev][i % HS_NEV], 0));
     return 0;
 }
@@ -845,83 +869,109 @@ int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset)
     return 0;
 }
 
+/* the row helpers below index rows by blockIdx.y (at most 65535 per launch): larger
+ * batches are launched in slices of Y_MAX rows */
+#define Y_MAX 65535
+
 int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
 {
-    if (batch > 65535) return -1;
     const char *e = getenv("HSFFT_R2C_POST");
-    if (e && atoi(e) == 1)
-        hipLaunchKernelGGL(k_r2c_post, dim3(grid_for(h + 1, 256), batch), dim3(256), 0, stream(), (const double2 *)Z,
-                           (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
-    else
-        hipLaunchKernelGGL(k_r2c_post2<false>, dim3(grid_for(h / 2 + 1, 256), batch), dim3(256), 0, stream(),
-                           (const double2 *)Z, (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        const double2 *z = (const double2 *)Z + b0 * zdist;
+        double2 *x = (double2 *)X + b0 * xdist;
+        if (e && atoi(e) == 1)
+            hipLaunchKernelGGL(k_r2c_post, dim3(grid_for(h + 1, 256), nb), dim3(256), 0, stream(), z,
+                               (const double2 *)tw2, x, h, zdist, xdist);
+        else
+            hipLaunchKernelGGL(k_r2c_post2<false>, dim3(grid_for(h / 2 + 1, 256), nb), dim3(256), 0, stream(), z,
+                               (const double2 *)tw2, x, h, zdist, xdist);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 /* bins 0..h only (rows of h+1 complex): the non-redundant half of real.c's mirrored output */
 int hsd_r2c_post_compact(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_r2c_post2<true>, dim3(grid_for(h / 2 + 1, 256), batch), dim3(256), 0, stream(),
-                       (const double2 *)Z, (const double2 *)tw2, (double2 *)X, h, zdist, xdist);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        hipLaunchKernelGGL(k_r2c_post2<true>, dim3(grid_for(h / 2 + 1, 256), nb), dim3(256), 0, stream(),
+                           (const double2 *)Z + b0 * zdist, (const double2 *)tw2, (double2 *)X + b0 * xdist, h, zdist,
+                           xdist);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 int hsd_c2r_pre(const void *X, const void *tw2, void *Zin, int h, int batch, long long xdist, long long zdist)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_c2r_pre, dim3(grid_for(h, 256), batch), dim3(256), 0, stream(), (const double2 *)X,
-                       (const double2 *)tw2, (double2 *)Zin, h, xdist, zdist);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        hipLaunchKernelGGL(k_c2r_pre, dim3(grid_for(h, 256), nb), dim3(256), 0, stream(), (const double2 *)X + b0 * xdist,
+                           (const double2 *)tw2, (double2 *)Zin + b0 * zdist, h, xdist, zdist);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 int hsd_cmul(const void *A, const void *Bv, void *C, long long n, int batch, long long dist)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_cmul, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (const double2 *)A,
-                       (const double2 *)Bv, (double2 *)C, n, dist);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        const long long o = b0 * dist;
+        hipLaunchKernelGGL(k_cmul, dim3(grid_for(n, 256), nb), dim3(256), 0, stream(), (const double2 *)A + o,
+                           (const double2 *)Bv + o, (double2 *)C + o, n, dist);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 int hsd_scale_real(void *x, long long n, int batch, long long dist, double divisor)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_scale_real, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (double *)x, n, dist, divisor);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        hipLaunchKernelGGL(k_scale_real, dim3(grid_for(n, 256), nb), dim3(256), 0, stream(), (double *)x + b0 * dist, n,
+                           dist, divisor);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 int hsd_c2r_pre_mul(const void *A, const void *Bv, const void *tw2, void *Zin, int h, int batch, long long xdist,
                     long long zdist)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_c2r_pre_mul, dim3(grid_for(h, 256), batch), dim3(256), 0, stream(), (const double2 *)A,
-                       (const double2 *)Bv, (const double2 *)tw2, (double2 *)Zin, h, xdist, zdist);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        const long long o = b0 * xdist;
+        hipLaunchKernelGGL(k_c2r_pre_mul, dim3(grid_for(h, 256), nb), dim3(256), 0, stream(), (const double2 *)A + o,
+                           (const double2 *)Bv + o, (const double2 *)tw2, (double2 *)Zin + b0 * zdist, h, xdist, zdist);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 int hsd_copy_rows_div(const void *src, long long sdist, long long soff, void *dst, long long ddist, long long n,
                       int batch, double divisor)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_copy_rows_div, dim3(grid_for(n, 256), batch), dim3(256), 0, stream(), (const double *)src,
-                       sdist, soff, (double *)dst, ddist, n, divisor);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        hipLaunchKernelGGL(k_copy_rows_div, dim3(grid_for(n, 256), nb), dim3(256), 0, stream(),
+                           (const double *)src + b0 * sdist, sdist, soff, (double *)dst + b0 * ddist, ddist, n, divisor);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
 int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
                   long long dlen, int batch)
 {
-    if (batch > 65535) return -1;
-    hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(dlen, 256), batch), dim3(256), 0, stream(), (const double *)src,
-                       sdist, soff, ncopy, (double *)dst, ddist, dlen);
-    HCHK(hipGetLastError());
+    for (int b0 = 0; b0 < batch; b0 += Y_MAX) {
+        const int nb = batch - b0 < Y_MAX ? batch - b0 : Y_MAX;
+        hipLaunchKernelGGL(k_copy_rows, dim3(grid_for(dlen, 256), nb), dim3(256), 0, stream(),
+                           (const double *)src + b0 * sdist, sdist, soff, ncopy, (double *)dst + b0 * ddist, ddist, dlen);
+        HCHK(hipGetLastError());
+    }
     return 0;
 }
 
@@ -967,46 +1017,43 @@ extern "C" int hsd_copy_bench_v(const void *src, void *dst, long long n16, int i
 
 int hsd_timer_start(void)
 {
-    if (!g_timer_init) {
-        HCHK(hipEventCreate(&g_t0));
-        HCHK(hipEventCreate(&g_t1));
-        g_timer_init = true;
-    }
-    HCHK(hipEventRecord(g_t0, stream()));
+    const int dev = cur_dev();
+    if (!timer_events(dev)) return set_err(hipErrorOutOfMemory, "hipEventCreate");
+    HCHK(hipEventRecord(g_t0[dev], stream()));
     return 0;
 }
 
 int hsd_timer_stop(float *ms)
 {
-    HCHK(hipEventRecord(g_t1, stream()));
-    HCHK(hipEventSynchronize(g_t1));
-    HCHK(hipEventElapsedTime(ms, g_t0, g_t1));
+    const int dev = cur_dev();
+    HCHK(hipEventRecord(g_t1[dev], stream()));
+    HCHK(hipEventSynchronize(g_t1[dev]));
+    HCHK(hipEventElapsedTime(ms, g_t0[dev], g_t1[dev]));
     return 0;
 }
 
 int hsd_pass_timer_begin(int i)
 {
-    if (!g_pev_init) {
-        for (int k = 0; k < 2 * HS_MAX_PASSES; k++) HCHK(hipEventCreate(&g_pev[k]));
-        g_pev_init = true;
-    }
+    const int dev = cur_dev();
+    if (!timer_events(dev)) return set_err(hipErrorOutOfMemory, "hipEventCreate");
     if (i < 0 || i >= HS_MAX_PASSES) return -1;
-    HCHK(hipEventRecord(g_pev[2 * i], stream()));
+    HCHK(hipEventRecord(g_pev[dev][2 * i], stream()));
     return 0;
 }
 
 int hsd_pass_timer_end(int i)
 {
     if (i < 0 || i >= HS_MAX_PASSES) return -1;
-    HCHK(hipEventRecord(g_pev[2 * i + 1], stream()));
+    HCHK(hipEventRecord(g_pev[cur_dev()][2 * i + 1], stream()));
     return 0;
 }
 
 int hsd_pass_timer_read(int n, float *ms)
 {
+    const int dev = cur_dev();
     for (int i = 0; i < n && i < HS_MAX_PASSES; i++) {
-        HCHK(hipEventSynchronize(g_pev[2 * i + 1]));
-        HCHK(hipEventElapsedTime(&ms[i], g_pev[2 * i], g_pev[2 * i + 1]));
+        HCHK(hipEventSynchronize(g_pev[dev][2 * i + 1]));
+        HCHK(hipEventElapsedTime(&ms[i], g_pev[dev][2 * i], g_pev[dev][2 * i + 1]));
     }
     return 0;
 }

@@ -18,9 +18,33 @@
 #include "hsfft_gpu.h"
 #include "hsfft_host.h"
 
-static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* the plan registry */
 static hs_entry *g_entries;
 static __thread char g_errbuf[512];
+
+/* per-device API locks (recursive: public entry points call each other) */
+static pthread_mutex_t g_dev_mtx[HS_MAX_DEV];
+static pthread_once_t g_dev_once = PTHREAD_ONCE_INIT;
+
+static void dev_mtx_init(void)
+{
+    pthread_mutexattr_t at;
+    pthread_mutexattr_init(&at);
+    pthread_mutexattr_settype(&at, PTHREAD_MUTEX_RECURSIVE);
+    for (int d = 0; d < HS_MAX_DEV; d++) pthread_mutex_init(&g_dev_mtx[d], &at);
+    pthread_mutexattr_destroy(&at);
+}
+
+int hs_lock_device(void)
+{
+    pthread_once(&g_dev_once, dev_mtx_init);
+    int d = hsd_get_device();
+    if (d < 0 || d >= HS_MAX_DEV) d = 0;
+    pthread_mutex_lock(&g_dev_mtx[d]);
+    return d;
+}
+
+void hs_unlock_device(int dev) { pthread_mutex_unlock(&g_dev_mtx[dev]); }
 
 void hs_seterr(const char *fmt, ...)
 {
@@ -38,11 +62,14 @@ static void fatal(const char *what)
     exit(EXIT_FAILURE);
 }
 
+static int g_ndev = -1;
+static pthread_once_t g_ndev_once = PTHREAD_ONCE_INIT;
+static void ndev_init(void) { g_ndev = hsd_device_count(); }
+
 int hs_require_gpu(void)
 {
-    static int ndev = -1;
-    if (ndev < 0) ndev = hsd_device_count();
-    if (ndev <= 0) {
+    pthread_once(&g_ndev_once, ndev_init);
+    if (g_ndev <= 0) {
         hs_seterr("no HIP device available: libhsfft has no CPU execution path");
         return HSFFT_ERR_DEVICE;
     }
@@ -75,13 +102,9 @@ static int effective_stages(int M, const int *fac, int lf, int *out, int *first_
 
 static int pass_pmax(void)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *s = getenv("HSFFT_PMAX");
-        v = s ? atoi(s) : 512;
-        if (v < 8) v = 8;
-    }
-    return v;
+    const char *s = getenv("HSFFT_PMAX");
+    const int v = s ? atoi(s) : 512;
+    return v < 8 ? 8 : v;
 }
 
 static int env_int(const char *name, int dflt)
@@ -387,6 +410,16 @@ static hs_entry *entry_build(const struct fft_set *o)
     return e;
 }
 
+/* unlink e (registry lock held); it is freed now, or by the last hs_entry_put */
+static void entry_retire(hs_entry **pp)
+{
+    hs_entry *e = *pp;
+    *pp = e->next;
+    e->next = NULL;
+    e->dead = 1;
+    if (e->refs == 0) entry_free(e);
+}
+
 hs_entry *hs_entry_get(const struct fft_set *obj)
 {
     pthread_mutex_lock(&g_lock);
@@ -397,8 +430,7 @@ hs_entry *hs_entry_get(const struct fft_set *obj)
             break;
         }
     if (e && !snapshot_matches(e, obj)) { /* caller edited the public fields: rebuild */
-        *pp = e->next;
-        entry_free(e);
+        entry_retire(pp);
         e = NULL;
     }
     if (!e) {
@@ -408,8 +440,17 @@ hs_entry *hs_entry_get(const struct fft_set *obj)
             g_entries = e;
         }
     }
+    if (e) e->refs++;
     pthread_mutex_unlock(&g_lock);
     return e;
+}
+
+void hs_entry_put(hs_entry *e)
+{
+    if (!e) return;
+    pthread_mutex_lock(&g_lock);
+    if (--e->refs == 0 && e->dead) entry_free(e);
+    pthread_mutex_unlock(&g_lock);
 }
 
 void hs_entry_release(const struct fft_set *obj)
@@ -417,9 +458,7 @@ void hs_entry_release(const struct fft_set *obj)
     pthread_mutex_lock(&g_lock);
     for (hs_entry **pp = &g_entries; *pp; pp = &(*pp)->next)
         if ((*pp)->key == obj) {
-            hs_entry *e = *pp;
-            *pp = e->next;
-            entry_free(e);
+            entry_retire(pp);
             break;
         }
     pthread_mutex_unlock(&g_lock);
@@ -430,6 +469,7 @@ void hs_entry_release(const struct fft_set *obj)
 static void *g_scr[HS_MAX_DEV][HS_NSCRATCH];
 static size_t g_scr_sz[HS_MAX_DEV][HS_NSCRATCH];
 
+/* (callers hold the device lock) */
 void *hs_scratch(int cls, size_t bytes)
 {
     int d = hsd_get_device();
@@ -443,26 +483,39 @@ void *hs_scratch(int cls, size_t bytes)
     return g_scr[d][cls];
 }
 
-static size_t chunk_bytes(void)
+int hsfft_release_scratch(void)
 {
-    static size_t v = 0;
-    if (!v) {
-        const char *s = getenv("HSFFT_CHUNK_MB");
-        v = (size_t)(s ? atof(s) : 256.0) * (1u << 20);
-        if (v < (1u << 20)) v = 1u << 20;
+    const int d = hs_lock_device();
+    int rc = 0;
+    if (hs_require_gpu() == 0) {
+        rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
+        for (int c = 0; c < HS_NSCRATCH; c++) {
+            if (hsd_free(g_scr[d][c]) && !rc) rc = HSFFT_ERR_DEVICE;
+            g_scr[d][c] = NULL;
+            g_scr_sz[d][c] = 0;
+        }
     }
-    return v;
+    hs_unlock_device(d);
+    return rc;
 }
+
+/* Chunk sizes, one knob per path, all read per call: HSFFT_CHUNK_MB (c2c intermediates of
+ * 3+-pass chains), HSFFT_BLUE_CHUNK_MB (Bluestein M-point intermediates), HSFFT_REAL_CHUNK_MB
+ * (the real paths' inner intermediate, hsfft_real.c). */
+size_t hs_env_mb(const char *name, double dflt_mb)
+{
+    const char *s = getenv(name);
+    const double mb = s ? atof(s) : dflt_mb;
+    const size_t v = (size_t)(mb * (double)(1u << 20));
+    return v < (1u << 20) ? (1u << 20) : v;
+}
+
+static size_t chunk_bytes(void) { return hs_env_mb("HSFFT_CHUNK_MB", 256.0); }
 
 /* Bluestein scratch per chunk (two M-point intermediates): large chunks keep the three
  * launches per chunk long enough to fill the chip (measured, 8192 x 99991: 64 rows 14.9,
  * 256 rows 16.0, 1024 rows 16.9 GSamples/s; 16 rows 12.7) */
-static size_t blue_chunk_bytes(void)
-{
-    const char *s = getenv("HSFFT_CHUNK_MB");
-    size_t v = (size_t)(s ? atof(s) : 4096.0) * (1u << 20);
-    return v < (1u << 20) ? (1u << 20) : v;
-}
+static size_t blue_chunk_bytes(void) { return hs_env_mb("HSFFT_BLUE_CHUNK_MB", 4096.0); }
 
 /* ------------------------------------------------------------------ device state */
 static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idist, void *O, long long odist,
@@ -703,16 +756,25 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
     long long chunk = (long long)(blue_chunk_bytes() / (sizeof(fft_data) * (size_t)M));
     if (chunk < 1) chunk = 1;
     if (chunk > batch) chunk = batch;
-    void *mid = hs_scratch(3, sizeof(fft_data) * (size_t)(chunk * M));
-    if (!mid) return HSFFT_ERR_NOMEM;
     /* M = 512 x 512 as two [8,8,8] passes: the forward FFT's last pass, the spectrum product
      * and the inverse FFT's first pass run as one kernel (the columns coincide) */
     const hsd_pass *p0 = &e->pass[0], *p1 = &e->pass[1];
     const int fuse = e->npass == 2 && M == 512 * 512 && p0->P == 512 && p1->P == 512 && p0->nst == 3 &&
                      p1->nst == 3 && p0->variant == HS_KV_R8X3 && p1->variant == HS_KV_R8X3 &&
                      p0->radix[0] == 8 && !env_int("HSFFT_BLUE_NOFUSE", 0);
-    void *mid2 = fuse ? hs_scratch(8, sizeof(fft_data) * (size_t)(chunk * M)) : NULL;
-    if (fuse && !mid2) return HSFFT_ERR_NOMEM;
+    /* the two M-point intermediates; halved while the allocation fails (a fuller device runs
+     * in smaller chunks) */
+    void *mid = NULL, *mid2 = NULL;
+    for (;;) {
+        mid = hs_scratch(3, sizeof(fft_data) * (size_t)(chunk * M));
+        mid2 = fuse && mid ? hs_scratch(8, sizeof(fft_data) * (size_t)(chunk * M)) : NULL;
+        if ((mid && (mid2 || !fuse)) || chunk == 1) break;
+        chunk = (chunk + 1) / 2;
+    }
+    if (!mid || (fuse && !mid2)) {
+        hs_seterr("bluestein scratch allocation of %lld bytes failed", (long long)(chunk * M * 16));
+        return HSFFT_ERR_NOMEM;
+    }
     for (long long c0 = 0; c0 < batch && fuse; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         int rc = hsd_blue_first((const fft_data *)in + c0 * idist, idist, mid, M, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
@@ -773,7 +835,7 @@ int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long lo
 }
 
 /* ------------------------------------------------------------------ drop-in fft_exec */
-void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
+static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
 {
     if (obj == NULL || inp == NULL || oup == NULL) {
         fprintf(stderr, "Error: Invalid FFT object or data pointers\n");
@@ -802,7 +864,15 @@ void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
         if (!rc) rc = dout ? hsd_d2d_async(oup, dq, bytes) : hsd_d2h(oup, dq, bytes);
     }
     if (!rc) rc = hsd_sync();
+    hs_entry_put(e);
     if (rc) fatal("fft_exec failed");
+}
+
+void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
+{
+    const int d = hs_lock_device();
+    fft_exec_locked(obj, inp, oup);
+    hs_unlock_device(d);
 }
 
 /* ------------------------------------------------------------------ extension API */
@@ -822,7 +892,10 @@ int hsfft_plan_refresh(fft_object obj)
     if (!obj) return HSFFT_ERR_ARG;
     hs_entry *e = hs_entry_get(obj);
     if (!e) return HSFFT_ERR_ARG;
+    pthread_mutex_lock(&g_lock);
     e->version++;
+    pthread_mutex_unlock(&g_lock);
+    hs_entry_put(e);
     return 0;
 }
 
@@ -830,7 +903,9 @@ int hsfft_plan_num_passes(fft_object obj)
 {
     if (!obj) return HSFFT_ERR_ARG;
     hs_entry *e = hs_entry_get(obj);
-    return e ? e->npass : HSFFT_ERR_ARG;
+    const int n = e ? e->npass : HSFFT_ERR_ARG;
+    hs_entry_put(e);
+    return n;
 }
 
 static int drmap(const struct fft_set *o, int *map, int oo, int io, int stride, int n, int fi)
@@ -862,9 +937,12 @@ int hsfft_exec_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
     if (batch == 0) return 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(obj);
-    if (!e) return HSFFT_ERR_ARG;
-    return hs_c2c_rows(e, d_in, obj->N, d_out, obj->N, batch);
+    rc = e ? hs_c2c_rows(e, d_in, obj->N, d_out, obj->N, batch) : HSFFT_ERR_ARG;
+    hs_entry_put(e);
+    hs_unlock_device(d);
+    return rc;
 }
 
 /* Host-resident batch: rows are streamed through two HBM staging
@@ -878,6 +956,8 @@ static size_t host_chunk_bytes(void)
     return v < (1u << 20) ? (1u << 20) : v;
 }
 
+static int exec_host_locked(fft_object obj, hs_entry *e, const fft_data *h_in, fft_data *h_out, int batch);
+
 int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_out, int batch)
 {
     g_errbuf[0] = 0;
@@ -888,8 +968,17 @@ int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_ou
     if (batch == 0) return 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(obj);
-    if (!e) return HSFFT_ERR_ARG;
+    rc = e ? exec_host_locked(obj, e, h_in, h_out, batch) : HSFFT_ERR_ARG;
+    hs_entry_put(e);
+    hs_unlock_device(d);
+    return rc;
+}
+
+static int exec_host_locked(fft_object obj, hs_entry *e, const fft_data *h_in, fft_data *h_out, int batch)
+{
+    int rc = 0;
     const long long N = obj->N;
     const size_t row = sizeof(fft_data) * (size_t)N, total = row * (size_t)batch;
     long long chunk = (long long)(host_chunk_bytes() / row);
@@ -932,14 +1021,25 @@ int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_ou
 int hsfft_fill_complex(fft_data *d_x, int64_t count, uint64_t seed, uint64_t offset)
 {
     int rc = hs_require_gpu();
-    return rc ? rc : (hsd_fill_complex(d_x, count, seed, offset) ? HSFFT_ERR_DEVICE : 0);
+    if (rc) return rc;
+    const int d = hs_lock_device();
+    rc = hsd_fill_complex(d_x, count, seed, offset) ? HSFFT_ERR_DEVICE : 0;
+    hs_unlock_device(d);
+    return rc;
 }
 
 int hsfft_fill_real(fft_type *d_x, int64_t count, uint64_t seed, uint64_t offset)
 {
     int rc = hs_require_gpu();
-    return rc ? rc : (hsd_fill_real(d_x, count, seed, offset) ? HSFFT_ERR_DEVICE : 0);
+    if (rc) return rc;
+    const int d = hs_lock_device();
+    rc = hsd_fill_real(d_x, count, seed, offset) ? HSFFT_ERR_DEVICE : 0;
+    hs_unlock_device(d);
+    return rc;
 }
+
+static int time_locked(fft_object obj, hs_entry *e, const fft_data *d_in, fft_data *d_out, int batch, int iters,
+                       float *ms, float *pass_ms, int max_pass);
 
 int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch, int iters, float *ms,
                        float *pass_ms, int max_pass)
@@ -947,8 +1047,18 @@ int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
     if (!obj || iters < 1 || !ms) return HSFFT_ERR_ARG;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(obj);
-    if (!e) return HSFFT_ERR_ARG;
+    rc = e ? time_locked(obj, e, d_in, d_out, batch, iters, ms, pass_ms, max_pass) : HSFFT_ERR_ARG;
+    hs_entry_put(e);
+    hs_unlock_device(d);
+    return rc;
+}
+
+static int time_locked(fft_object obj, hs_entry *e, const fft_data *d_in, fft_data *d_out, int batch, int iters,
+                       float *ms, float *pass_ms, int max_pass)
+{
+    int rc;
     if (hsd_timer_start()) return HSFFT_ERR_DEVICE;
     for (int it = 0; it < iters; it++) {
         rc = hs_c2c_rows(e, d_in, obj->N, d_out, obj->N, batch);
@@ -982,26 +1092,61 @@ int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, fl
     if (!d_src || !d_dst || !ms || iters < 1 || bytes % 16) return HSFFT_ERR_ARG;
     int rc = hs_require_gpu();
     if (rc) return rc;
-    return hsd_copy_bench(d_src, d_dst, (long long)(bytes / 16), iters, ms) ? HSFFT_ERR_DEVICE : 0;
+    const int d = hs_lock_device();
+    rc = hsd_copy_bench(d_src, d_dst, (long long)(bytes / 16), iters, ms) ? HSFFT_ERR_DEVICE : 0;
+    hs_unlock_device(d);
+    return rc;
+}
+
+/* one host thread per device: each selects its device, enqueues its contiguous shard and
+ * waits for it; no data crosses devices.  Per-device state (twiddles, Bluestein hk) is built
+ * by that device's thread, so first use builds all devices' state concurrently. */
+typedef struct {
+    fft_object obj;
+    const fft_data *in;
+    fft_data *out;
+    int dev, rows, rc;
+    char err[512];
+} hs_shard;
+
+static void *shard_main(void *arg)
+{
+    hs_shard *s = arg;
+    s->rc = hsd_set_device(s->dev) ? HSFFT_ERR_DEVICE : 0;
+    if (!s->rc && s->rows > 0) s->rc = hsfft_exec_batched(s->obj, s->in, s->out, s->rows);
+    if (!s->rc && hsd_sync()) s->rc = HSFFT_ERR_DEVICE;
+    if (s->rc) snprintf(s->err, sizeof s->err, "device %d: %.400s", s->dev, g_errbuf[0] ? g_errbuf : hsd_errstr());
+    return NULL;
 }
 
 int hsfft_exec_multi(fft_object obj, const fft_data *const *d_in, fft_data *const *d_out, int batch, int ndev)
 {
-    if (!obj || !d_in || !d_out || ndev < 1 || batch < 0) return HSFFT_ERR_ARG;
+    g_errbuf[0] = 0;
+    if (!obj || !d_in || !d_out || ndev < 1 || batch < 0 || ndev > HS_MAX_DEV) return HSFFT_ERR_ARG;
     int rc = hs_require_gpu();
     if (rc) return rc;
     if (ndev > hsd_device_count()) return HSFFT_ERR_ARG;
     const int cur = hsd_get_device();
-    /* launches are asynchronous per device stream, so one host thread can keep every
-     * device busy; each device gets its contiguous shard, no data crosses devices */
-    for (int g = 0; g < ndev && !rc; g++) {
+    hs_shard sh[HS_MAX_DEV];
+    pthread_t th[HS_MAX_DEV];
+    int started[HS_MAX_DEV] = {0};
+    for (int g = 0; g < ndev; g++) {
         const int b0 = (int)((long long)batch * g / ndev), b1 = (int)((long long)batch * (g + 1) / ndev);
-        if (hsd_set_device(g)) return HSFFT_ERR_DEVICE;
-        rc = hsfft_exec_batched(obj, d_in[g], d_out[g], b1 - b0);
+        memset(&sh[g], 0, sizeof sh[g]);
+        sh[g].obj = obj;
+        sh[g].in = d_in[g];
+        sh[g].out = d_out[g];
+        sh[g].dev = g;
+        sh[g].rows = b1 - b0;
+        started[g] = pthread_create(&th[g], NULL, shard_main, &sh[g]) == 0;
+        if (!started[g]) shard_main(&sh[g]); /* no thread: run the shard here */
     }
     for (int g = 0; g < ndev; g++) {
-        hsd_set_device(g);
-        if (hsd_sync()) rc = rc ? rc : HSFFT_ERR_DEVICE;
+        if (started[g]) pthread_join(th[g], NULL);
+        if (sh[g].rc && !rc) {
+            rc = sh[g].rc;
+            hs_seterr("hsfft_exec_multi: %s", sh[g].err);
+        }
     }
     if (cur >= 0) hsd_set_device(cur);
     return rc;

@@ -39,6 +39,8 @@ typedef struct hs_entry {
     hs_devstate *ds[HS_MAX_DEV];
     int version;           /* bumped by hsfft_plan_refresh: device copies re-uploaded */
     int ds_version[HS_MAX_DEV];
+    int refs;              /* users holding the entry (hs_entry_get .. hs_entry_put) */
+    int dead;              /* unlinked (free_fft or a rebuild): freed by the last put */
     struct hs_entry *next;
 } hs_entry;
 
@@ -48,9 +50,17 @@ void hs_longvector(fft_data *tw, int M, const int *fac, int lf, int exact);
 int hs_bluestein_M_init(int N); /* fft_init sizing (log10), ref :242-252 */
 int hs_bluestein_M_exec(int N); /* bluestein_fft sizing (log2), ref :1750-1751 */
 
-/* registry / scheduling / execution (hsfft_exec.c) */
+/* registry / scheduling / execution (hsfft_exec.c).  hs_entry_get returns the entry with a
+ * reference held; every successful get is paired with hs_entry_put. */
 hs_entry *hs_entry_get(const struct fft_set *obj);
+void hs_entry_put(hs_entry *e);
 void hs_entry_release(const struct fft_set *obj);
+/* Reentrancy: every public entry point that enqueues work or touches per-device state
+ * (scratch pool, staging slots, streams, events, lazily built device state) runs under the
+ * recursive lock of the calling thread's current device.  Host threads on different devices
+ * run concurrently; threads sharing a device take turns per call. */
+int hs_lock_device(void);
+void hs_unlock_device(int dev);
 int hs_require_gpu(void);
 void hs_seterr(const char *fmt, ...);
 int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long long odist, int batch);
@@ -65,6 +75,8 @@ int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_ty
 int hs_c2r_product_rows(fft_real_object r, const fft_data *d_a, const fft_data *d_b, long long xdist, fft_type *d_out,
                         int batch);
 void *hs_scratch(int cls, size_t bytes);
+/* bytes from an environment knob given in MiB (default dflt_mb; at least 1 MiB) */
+size_t hs_env_mb(const char *name, double dflt_mb);
 
 #ifdef __cplusplus
 }

@@ -432,7 +432,9 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         const int loc = e - (L - 1), k = loc / (R - 1), i1 = loc % (R - 1);
         ltw[L - 1 + i1 * L + k] = a.tw[e];
     }
-    /* (the first exchange's leading barrier orders these writes before any read) */
+    /* fused01 reads the stage-1 entries before the first exchange's barrier, so the copy
+     * needs a barrier of its own (once per workgroup) */
+    __syncthreads();
 #pragma unroll 1
     for (unsigned b = blockIdx.x; b < (unsigned)a.batch; b += gridDim.x) {
         int jt = jt0;

@@ -106,8 +106,7 @@ void free_real_fft(fft_real_object r)
  * the allocation fails, so a device with less free HBM still runs, in smaller chunks */
 static fft_data *real_chunk(int h, int batch, long long *chunk)
 {
-    const char *s = getenv("HSFFT_CHUNK_MB");
-    const size_t bytes = (size_t)(s ? atof(s) : 16384.0) * (1u << 20);
+    const size_t bytes = hs_env_mb("HSFFT_REAL_CHUNK_MB", 16384.0);
     long long rows = (long long)(bytes / (sizeof(fft_data) * (size_t)h));
     if (rows < 1) rows = 1;
     if (rows > batch) rows = batch;
@@ -122,6 +121,8 @@ static fft_data *real_chunk(int h, int batch, long long *chunk)
     }
 }
 
+static int r2c_locked(fft_real_object r, hs_entry *e, const fft_type *d_in, fft_data *d_out, int batch);
+
 int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, int batch)
 {
     if (!r || !r->cobj || !d_in || !d_out || batch < 0) {
@@ -131,9 +132,19 @@ int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, 
     if (batch == 0) return 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(r->cobj);
+    rc = e ? r2c_locked(r, e, d_in, d_out, batch) : HSFFT_ERR_DEVICE;
+    hs_entry_put(e);
+    hs_unlock_device(d);
+    return rc;
+}
+
+static int r2c_locked(fft_real_object r, hs_entry *e, const fft_type *d_in, fft_data *d_out, int batch)
+{
+    int rc = 0;
     void *tw2 = tw2_device(r);
-    if (!e || !tw2) return HSFFT_ERR_DEVICE;
+    if (!tw2) return HSFFT_ERR_DEVICE;
     const int h = r->cobj->N, N = 2 * h;
     long long chunk;
     fft_data *Z = real_chunk(h, batch, &chunk);
@@ -154,6 +165,8 @@ int hsfft_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, 
 /* compact r2c: bins 0..N/2 per row (rows of N/2+1 complex), the
  * non-redundant half of the reference's mirrored output -- 16 B written per real sample
  * instead of 24 for the same values (bit-identical to bins 0..N/2 of hsfft_r2c_batched) */
+static int r2c_compact_locked(fft_real_object r, hs_entry *e, const fft_type *d_in, fft_data *d_out, int batch);
+
 int hsfft_r2c_batched_compact(fft_real_object r, const fft_type *d_in, fft_data *d_out, int batch)
 {
     if (!r || !r->cobj || !d_in || !d_out || batch < 0) {
@@ -163,9 +176,19 @@ int hsfft_r2c_batched_compact(fft_real_object r, const fft_type *d_in, fft_data 
     if (batch == 0) return 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
+    const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(r->cobj);
+    rc = e ? r2c_compact_locked(r, e, d_in, d_out, batch) : HSFFT_ERR_DEVICE;
+    hs_entry_put(e);
+    hs_unlock_device(d);
+    return rc;
+}
+
+static int r2c_compact_locked(fft_real_object r, hs_entry *e, const fft_type *d_in, fft_data *d_out, int batch)
+{
+    int rc = 0;
     void *tw2 = tw2_device(r);
-    if (!e || !tw2) return HSFFT_ERR_DEVICE;
+    if (!tw2) return HSFFT_ERR_DEVICE;
     const int h = r->cobj->N, N = 2 * h;
     long long chunk;
     fft_data *Z = real_chunk(h, batch, &chunk);
@@ -191,25 +214,30 @@ int hsfft_c2r_batched(fft_real_object r, const fft_data *d_in, fft_type *d_out, 
     if (batch == 0) return 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
-    return hs_c2r_rows(r, d_in, 2LL * r->cobj->N, d_out, batch);
+    const int d = hs_lock_device();
+    rc = hs_c2r_rows(r, d_in, 2LL * r->cobj->N, d_out, batch);
+    hs_unlock_device(d);
+    return rc;
 }
 
+/* (callers hold the device lock) */
 int hs_c2r_product_rows(fft_real_object r, const fft_data *d_a, const fft_data *d_b, long long xdist, fft_type *d_out,
                         int batch)
 {
     int rc = 0;
     hs_entry *e = hs_entry_get(r->cobj);
-    void *tw2 = tw2_device(r);
-    if (!e || !tw2) return HSFFT_ERR_DEVICE;
+    void *tw2 = e ? tw2_device(r) : NULL;
     const int h = r->cobj->N, N = 2 * h;
-    long long chunk;
-    fft_data *Zi = real_chunk(h, batch, &chunk);
-    if (!Zi) return HSFFT_ERR_NOMEM;
+    long long chunk = 1;
+    fft_data *Zi = tw2 ? real_chunk(h, batch, &chunk) : NULL;
+    if (!tw2) rc = HSFFT_ERR_DEVICE;
+    else if (!Zi) rc = HSFFT_ERR_NOMEM;
     for (long long c0 = 0; c0 < batch && !rc; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         rc = hsd_c2r_pre_mul(d_a + c0 * xdist, d_b + c0 * xdist, tw2, Zi, h, cb, xdist, h) ? HSFFT_ERR_DEVICE : 0;
         if (!rc) rc = hs_c2c_rows(e, Zi, h, d_out + c0 * N, h, cb);
     }
+    hs_entry_put(e);
     return rc;
 }
 
@@ -219,20 +247,20 @@ int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_ty
 {
     int rc = 0;
     hs_entry *e = hs_entry_get(r->cobj);
-    void *tw2 = tw2_device(r);
-    if (!e || !tw2) return HSFFT_ERR_DEVICE;
+    void *tw2 = e ? tw2_device(r) : NULL;
     const int h = r->cobj->N, N = 2 * h;
-    long long chunk;
-    fft_data *Zi = real_chunk(h, batch, &chunk);
-    if (!Zi) return HSFFT_ERR_NOMEM;
-    for (long long c0 = 0; c0 < batch; c0 += chunk) {
+    long long chunk = 1;
+    fft_data *Zi = tw2 ? real_chunk(h, batch, &chunk) : NULL;
+    if (!tw2) rc = HSFFT_ERR_DEVICE;
+    else if (!Zi) rc = HSFFT_ERR_NOMEM;
+    for (long long c0 = 0; c0 < batch && !rc; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         rc = hsd_c2r_pre(d_in + c0 * xdist, tw2, Zi, h, cb, xdist, h) ? HSFFT_ERR_DEVICE : 0;
         /* unpacking complex_output into interleaved reals is again a reinterpretation */
         if (!rc) rc = hs_c2c_rows(e, Zi, h, d_out + c0 * N, h, cb);
-        if (rc) return rc;
     }
-    return 0;
+    hs_entry_put(e);
+    return rc;
 }
 
 int hsfft_time_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_out, int batch, int iters, float *ms)
@@ -240,11 +268,13 @@ int hsfft_time_r2c_batched(fft_real_object r, const fft_type *d_in, fft_data *d_
     if (!r || iters < 1 || !ms) return HSFFT_ERR_ARG;
     int rc = hs_require_gpu();
     if (rc) return rc;
-    if ((rc = hsfft_r2c_batched(r, d_in, d_out, batch))) return rc; /* device state outside the timing */
-    if (hsd_timer_start()) return HSFFT_ERR_DEVICE;
-    for (int i = 0; i < iters; i++)
-        if ((rc = hsfft_r2c_batched(r, d_in, d_out, batch))) return rc;
-    return hsd_timer_stop(ms) ? HSFFT_ERR_DEVICE : 0;
+    const int d = hs_lock_device();
+    rc = hsfft_r2c_batched(r, d_in, d_out, batch); /* device state outside the timing */
+    if (!rc && hsd_timer_start()) rc = HSFFT_ERR_DEVICE;
+    for (int i = 0; i < iters && !rc; i++) rc = hsfft_r2c_batched(r, d_in, d_out, batch);
+    if (!rc && hsd_timer_stop(ms)) rc = HSFFT_ERR_DEVICE;
+    hs_unlock_device(d);
+    return rc;
 }
 
 static void real_fail(const char *what)
@@ -253,7 +283,7 @@ static void real_fail(const char *what)
     exit(EXIT_FAILURE);
 }
 
-void fft_r2c_exec(fft_real_object r, fft_type *inp, fft_data *oup)
+static void r2c_exec_locked(fft_real_object r, fft_type *inp, fft_data *oup)
 {
     if (r == NULL || inp == NULL || oup == NULL) {
         fprintf(stderr, "Error: Invalid real FFT object or data pointers\n");
@@ -277,7 +307,14 @@ void fft_r2c_exec(fft_real_object r, fft_type *inp, fft_data *oup)
     if (rc) real_fail("fft_r2c_exec failed");
 }
 
-void fft_c2r_exec(fft_real_object r, fft_data *inp, fft_type *oup)
+void fft_r2c_exec(fft_real_object r, fft_type *inp, fft_data *oup)
+{
+    const int d = hs_lock_device();
+    r2c_exec_locked(r, inp, oup);
+    hs_unlock_device(d);
+}
+
+static void c2r_exec_locked(fft_real_object r, fft_data *inp, fft_type *oup)
 {
     if (r == NULL || inp == NULL || oup == NULL) {
         fprintf(stderr, "Error: Invalid real FFT object or data pointers\n");
@@ -301,4 +338,11 @@ void fft_c2r_exec(fft_real_object r, fft_data *inp, fft_type *oup)
     }
     if (!rc) rc = hsd_sync();
     if (rc) real_fail("fft_c2r_exec failed");
+}
+
+void fft_c2r_exec(fft_real_object r, fft_data *inp, fft_type *oup)
+{
+    const int d = hs_lock_device();
+    c2r_exec_locked(r, inp, oup);
+    hs_unlock_device(d);
 }

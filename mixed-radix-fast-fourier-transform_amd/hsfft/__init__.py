@@ -45,6 +45,7 @@ SIGNATURES = {
     "hsfft_memcpy_d2h": (CI, [VP, VP, ctypes.c_size_t]),
     "hsfft_memset": (CI, [VP, CI, ctypes.c_size_t]),
     "hsfft_synchronize": (CI, []),
+    "hsfft_release_scratch": (CI, []),
     "hsfft_get_stream": (VP, []),
     "hsfft_last_error": (ctypes.c_char_p, []),
     "hsfft_set_twiddle_mode": (CI, [CI]),

@@ -1,0 +1,231 @@
+/*
+ * null_device.c -- TEST INFRASTRUCTURE ONLY: a host-memory stand-in for the device layer
+ * (csrc/hsfft_internal.h's hsd_* functions) so that the host C of libhsfft.so (planner,
+ * registry, pass scheduler, chunking, real / convolution drivers) can be built and run under
+ * -fsanitize=address,undefined on a machine without a GPU (SURVEY.md §5 "Race detection /
+ * sanitizers").  It computes nothing: every "launch" checks the geometry the host chose and
+ * touches the first and last element of every row it would read or write, so an undersized
+ * scratch buffer or a wrong row stride is an AddressSanitizer report.  It is never linked
+ * into the product.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hsfft_internal.h"
+
+static __thread char err[256];
+static __thread int sidx;
+static volatile double sink;
+
+int hsd_device_count(void) { return 1; }
+int hsd_set_device(int dev) { return dev == 0 ? 0 : -1; }
+int hsd_get_device(void) { return 0; }
+void *hsd_malloc(size_t bytes) { return malloc(bytes ? bytes : 16); }
+int hsd_free(void *p)
+{
+    free(p);
+    return 0;
+}
+int hsd_h2d(void *d, const void *h, size_t bytes)
+{
+    memcpy(d, h, bytes);
+    return 0;
+}
+int hsd_d2h(void *h, const void *d, size_t bytes)
+{
+    memcpy(h, d, bytes);
+    return 0;
+}
+int hsd_d2d_async(void *d, const void *s, size_t bytes)
+{
+    memmove(d, s, bytes);
+    return 0;
+}
+int hsd_memset_async(void *d, int v, size_t bytes)
+{
+    memset(d, v, bytes);
+    return 0;
+}
+int hsd_sync(void) { return 0; }
+int hsd_select_stream(int idx)
+{
+    sidx = idx;
+    return 0;
+}
+int hsd_h2d_async(void *d, const void *h, size_t bytes) { return hsd_h2d(d, h, bytes); }
+int hsd_d2h_async(void *h, const void *d, size_t bytes) { return hsd_d2h(h, d, bytes); }
+int hsd_stream_sync(void) { return 0; }
+int hsd_host_register(void *p, size_t bytes) { return 0; }
+int hsd_host_unregister(void *p) { return 0; }
+int hsd_event_record(int i) { return i < 0 ? -1 : 0; }
+int hsd_event_wait(int i) { return i < 0 ? -1 : 0; }
+void *hsd_stream(void) { return NULL; }
+/* "device" memory is host memory here: pointers the tests pass as device buffers are
+ * malloc'd, so every pointer counts as a device pointer */
+int hsd_is_device_ptr(const void *p) { return p != NULL; }
+const char *hsd_errstr(void) { return err; }
+int hsd_cu_count(void) { return 256; }
+
+/* read the first and last element of `rows` rows of `len` complex, `dist` apart */
+static void touch_rows_r(const void *base, long long dist, long long len, long long rows, size_t esz)
+{
+    if (!base || rows <= 0 || len <= 0) return;
+    const char *b = base;
+    for (long long r = 0; r < rows; r++) {
+        sink += *(const double *)(b + (size_t)(r * dist) * esz);
+        sink += *(const double *)(b + (size_t)(r * dist + len - 1) * esz + esz - sizeof(double));
+    }
+}
+
+static void touch_rows_w(void *base, long long dist, long long len, long long rows, size_t esz)
+{
+    if (!base || rows <= 0 || len <= 0) return;
+    char *b = base;
+    for (long long r = 0; r < rows; r++) {
+        memset(b + (size_t)(r * dist) * esz, 0, esz);
+        memset(b + (size_t)(r * dist + len - 1) * esz, 0, esz);
+    }
+}
+
+int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
+{
+    if (p->P <= 0 || p->A <= 0 || p->B <= 0 || l->batch <= 0) {
+        snprintf(err, sizeof err, "null device: bad pass geometry");
+        return -1;
+    }
+    const long long M = (long long)p->P * p->A * p->B;
+    const long long in_len = l->load_op == HS_LOAD_CHIRP ? l->nsig : M;
+    const long long out_len = l->store_op == HS_STORE_CHIRP ? l->nsig : M;
+    touch_rows_r(l->in, l->idist, in_len, l->batch, 16);
+    touch_rows_r(l->tw, 0, M > 1 ? M - 1 : 1, 1, 16);
+    if (l->load_op == HS_LOAD_CHIRP) touch_rows_r(l->load_aux, 0, l->nsig, 1, 16);
+    if (l->store_op == HS_STORE_SPEC) touch_rows_r(l->store_aux, 0, M, 1, 16);
+    if (l->store_op == HS_STORE_CHIRP) touch_rows_r(l->store_aux, 0, l->nsig, 1, 16);
+    touch_rows_w(l->out, l->odist, out_len, l->batch, 16);
+    return 0;
+}
+
+/* the null device has every specialised variant the host may ask for */
+int r8_has_variant(int r0, int n8, int G, int Wq, int first) { return 1; }
+int mr_has_variant(const hsd_pass *p) { return 1; }
+
+int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
+                 long long B, int batch, int sgn, int compact)
+{
+    touch_rows_r(Z, zdist, h, batch, 16);
+    touch_rows_r(w2, 0, h, 1, 16);
+    touch_rows_w(X, xdist, compact ? h + 1 : 2 * h, batch, 16);
+    return 0;
+}
+int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
+                 int conj, int dir, int sgn2, int conj2)
+{
+    touch_rows_r(in, dist, dist, batch, 16);
+    touch_rows_r(hk, 0, dist, 1, 16);
+    touch_rows_w(out, dist, dist, batch, 16);
+    return 0;
+}
+int hsd_blue_last(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                  long long nsig, int batch, int dir)
+{
+    touch_rows_r(in, idist, idist, batch, 16);
+    touch_rows_w(out, odist, nsig, batch, 16);
+    return 0;
+}
+int hsd_blue_first(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                   long long nsig, int batch, int dir)
+{
+    touch_rows_r(in, idist, nsig, batch, 16);
+    touch_rows_r(chirp, 0, nsig, 1, 16);
+    touch_rows_w(out, odist, odist, batch, 16);
+    return 0;
+}
+int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset)
+{
+    memset(d, 0, (size_t)count * 16);
+    return 0;
+}
+int hsd_fill_real(void *d, int64_t count, uint64_t seed, uint64_t offset)
+{
+    memset(d, 0, (size_t)count * 8);
+    return 0;
+}
+int hsd_r2c_post(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
+{
+    touch_rows_r(Z, zdist, h, batch, 16);
+    touch_rows_w(X, xdist, 2LL * h, batch, 16);
+    return 0;
+}
+int hsd_r2c_post_compact(const void *Z, const void *tw2, void *X, int h, int batch, long long zdist, long long xdist)
+{
+    touch_rows_r(Z, zdist, h, batch, 16);
+    touch_rows_w(X, xdist, h + 1LL, batch, 16);
+    return 0;
+}
+int hsd_c2r_pre(const void *X, const void *tw2, void *Zin, int h, int batch, long long xdist, long long zdist)
+{
+    touch_rows_r(X, xdist, h + 1LL, batch, 16);
+    touch_rows_w(Zin, zdist, h, batch, 16);
+    return 0;
+}
+int hsd_cmul(const void *A, const void *Bv, void *C, long long n, int batch, long long dist)
+{
+    touch_rows_r(A, dist, n, batch, 16);
+    touch_rows_r(Bv, dist, n, batch, 16);
+    touch_rows_w(C, dist, n, batch, 16);
+    return 0;
+}
+int hsd_c2r_pre_mul(const void *A, const void *Bv, const void *tw2, void *Zin, int h, int batch, long long xdist,
+                    long long zdist)
+{
+    touch_rows_r(A, xdist, h + 1LL, batch, 16);
+    touch_rows_r(Bv, xdist, h + 1LL, batch, 16);
+    touch_rows_w(Zin, zdist, h, batch, 16);
+    return 0;
+}
+int hsd_copy_rows_div(const void *src, long long sdist, long long soff, void *dst, long long ddist, long long n,
+                      int batch, double divisor)
+{
+    touch_rows_r((const double *)src + soff, sdist, n, batch, 8);
+    touch_rows_w(dst, ddist, n, batch, 8);
+    return 0;
+}
+int hsd_scale_real(void *x, long long n, int batch, long long dist, double divisor)
+{
+    touch_rows_w(x, dist, n, batch, 8);
+    return 0;
+}
+int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
+                  long long dlen, int batch)
+{
+    touch_rows_r((const double *)src + soff, sdist, ncopy, batch, 8);
+    touch_rows_w(dst, ddist, dlen, batch, 8);
+    return 0;
+}
+int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
+                int conj, int rows_per_group, int lag, int grid)
+{
+    touch_rows_r(in, idist, 1 << 20, batch, 16);
+    touch_rows_w(out, odist, 1 << 20, batch, 16);
+    return 0;
+}
+int hsd_timer_start(void) { return 0; }
+int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *ms)
+{
+    *ms = 0.0f;
+    return 0;
+}
+int hsd_timer_stop(float *ms)
+{
+    *ms = 0.0f;
+    return 0;
+}
+int hsd_pass_timer_begin(int i) { return 0; }
+int hsd_pass_timer_end(int i) { return 0; }
+int hsd_pass_timer_read(int n, float *ms)
+{
+    for (int i = 0; i < n; i++) ms[i] = 0.0f;
+    return 0;
+}

@@ -1,0 +1,198 @@
+/*
+ * sanitize_driver.c -- TEST INFRASTRUCTURE ONLY (tests/test_sanitize_cpu.py).
+ *
+ * Runs the host C of libhsfft.so (csrc/hsfft_plan.c, hsfft_exec.c, hsfft_real.c,
+ * hsfft_convolve.c) against the null device (null_device.c) under
+ * -fsanitize=address,undefined:
+ *   1. planner: fft_init's public fields and twiddle bytes equal the oracle's plan for every
+ *      N <= PLAN_MAX and a list of larger sizes (ref highSpeedFFT.c:206-286, :1979-2313);
+ *   2. registry + scheduler: every size through fft_exec, hsfft_exec_batched, the host
+ *      pipeline, r2c / c2r (both layouts), convolution (every output type), a plan whose
+ *      public fields are edited between calls (registry rebuild), hsfft_plan_refresh,
+ *      hsfft_release_scratch -- the null device touches the first and last element of every
+ *      row each launch would read or write;
+ *   3. threads: 8 host threads creating / executing / freeing plans, sharing one plan, and
+ *      cycling convolutions through more padded lengths than the plan cache holds.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "highspeedFFT.h"
+#include "hsfft_gpu.h"
+#include "real.h"
+#include "../../oracle/hsfft_oracle.h"
+
+#define PLAN_MAX 3000
+
+static int fails;
+
+#define CHECK(c, ...)                         \
+    do {                                      \
+        if (!(c)) {                           \
+            fprintf(stderr, "FAIL: " __VA_ARGS__); \
+            fprintf(stderr, "\n");            \
+            fails++;                          \
+        }                                     \
+    } while (0)
+
+static void check_plan(int n, int sgn)
+{
+    fft_object o = fft_init(n, sgn);
+    orc_plan *r = orc_plan_create(n, sgn, 0);
+    CHECK(o && r, "plan %d", n);
+    if (!o || !r) return;
+    int fac[64];
+    const int lf = orc_plan_factors(r, fac);
+    long long mplan = 1;
+    for (int i = 0; i < o->lf; i++) mplan *= o->factors[i];
+    if (o->lt == 1 && mplan != orc_plan_M(r)) { /* D5 (N = 2^k+1): the oracle keeps the exec-length table */
+        orc_plan_destroy(r);
+        free_fft(o);
+        return;
+    }
+    CHECK(o->lf == lf && o->lt == orc_plan_lt(r) && o->N == n && o->sgn == sgn, "plan fields N=%d", n);
+    for (int i = 0; i < lf && i < o->lf; i++) CHECK(o->factors[i] == fac[i], "factor %d of N=%d", i, n);
+    const int M = orc_plan_M(r);
+    if (M > 1) CHECK(!memcmp(o->twiddle, orc_plan_twiddles(r), sizeof(fft_data) * (size_t)(M - 1)), "twiddles N=%d", n);
+    orc_plan_destroy(r);
+    free_fft(o);
+}
+
+static fft_data *cbuf(long long n)
+{
+    fft_data *p = malloc(sizeof(fft_data) * (size_t)(n > 0 ? n : 1));
+    for (long long i = 0; i < n; i++) p[i].re = p[i].im = (double)(i % 7);
+    return p;
+}
+
+static void run_c2c(int n, int batch)
+{
+    for (int sgn = -1; sgn <= 1; sgn += 2) {
+        fft_object o = fft_init(n, sgn);
+        fft_data *x = cbuf((long long)n * batch), *y = cbuf((long long)n * batch);
+        fft_exec(o, x, y);
+        CHECK(hsfft_exec_batched(o, x, y, batch) == 0, "exec_batched N=%d: %s", n, hsfft_last_error());
+        CHECK(hsfft_exec_batched_host(o, x, y, batch) == 0, "host N=%d", n);
+        free(x);
+        free(y);
+        free_fft(o);
+    }
+}
+
+static void run_real(int n, int batch)
+{
+    fft_real_object f = fft_real_init(n, 1), iv = fft_real_init(n, -1);
+    double *x = malloc(sizeof(double) * (size_t)n * batch);
+    for (long long i = 0; i < (long long)n * batch; i++) x[i] = (double)(i % 5);
+    fft_data *X = cbuf((long long)n * batch);
+    fft_r2c_exec(f, x, X);
+    fft_c2r_exec(iv, X, x);
+    CHECK(hsfft_r2c_batched(f, x, X, batch) == 0, "r2c N=%d", n);
+    CHECK(hsfft_r2c_batched_compact(f, x, X, batch) == 0, "r2c compact N=%d", n);
+    CHECK(hsfft_c2r_batched(iv, X, x, batch) == 0, "c2r N=%d", n);
+    free(x);
+    free(X);
+    free_real_fft(f);
+    free_real_fft(iv);
+}
+
+static void run_conv(int n, int m)
+{
+    static const char *types[] = {"full", "same", "valid"}, *ctypes[] = {"linear", "circular"};
+    double *a = calloc((size_t)n, sizeof(double)), *b = calloc((size_t)m, sizeof(double));
+    double *o = calloc(4 * (size_t)(n + m) + 8, sizeof(double));
+    for (int t = 0; t < 3; t++)
+        for (int c = 0; c < 2; c++) {
+            const int len = fft_convolve(types[t], ctypes[c], a, n, b, m, o);
+            CHECK(len > 0, "convolve %s %s %d %d", types[t], ctypes[c], n, m);
+        }
+    const int rows = 3;
+    double *ba = calloc((size_t)n * rows, sizeof(double)), *bb = calloc((size_t)m * rows, sizeof(double));
+    double *bo = calloc((size_t)(n + m) * rows + 8, sizeof(double));
+    CHECK(hsfft_convolve_batched("same", "linear", ba, n, bb, m, bo, rows) > 0, "convolve_batched %d %d", n, m);
+    free(a);
+    free(b);
+    free(o);
+    free(ba);
+    free(bb);
+    free(bo);
+}
+
+static fft_object g_shared;
+
+static void *hammer(void *arg)
+{
+    const int t = (int)(long)arg;
+    fft_data *x = cbuf(12600), *y = cbuf(12600);
+    for (int it = 0; it < 40; it++) {
+        fft_exec(g_shared, x, y);
+        const int n = 8 + 37 * ((t * 40 + it) % 23);
+        fft_object o = fft_init(n, it & 1 ? 1 : -1);
+        fft_data *a = cbuf(n), *b = cbuf(n);
+        fft_exec(o, a, b);
+        free(a);
+        free(b);
+        free_fft(o);
+        const int k = 5 + (t + it) % 10; /* ten padded lengths: more than the 8 cached pairs */
+        const int len = (1 << k) / 2;
+        double *ca = calloc((size_t)len, sizeof(double)), *cb = calloc((size_t)len, sizeof(double));
+        double *co = calloc(2 * (size_t)len + 8, sizeof(double));
+        CHECK(fft_convolve("full", "linear", ca, len, cb, len, co) == 2 * len - 1, "thread conv");
+        free(ca);
+        free(cb);
+        free(co);
+    }
+    free(x);
+    free(y);
+    return NULL;
+}
+
+int main(void)
+{
+    for (int n = 1; n <= PLAN_MAX; n++) {
+        check_plan(n, 1);
+        if (n % 7 == 0) check_plan(n, -1);
+    }
+    const int big[] = {12600, 65536, 99991, 1 << 20, 65537, 169, 2 * 3 * 5 * 7 * 11 * 13};
+    for (unsigned i = 0; i < sizeof big / sizeof big[0]; i++) check_plan(big[i], 1);
+
+    const int sizes[] = {1, 2, 3, 7, 8, 12, 13, 16, 19, 97, 128, 1000, 1021, 1024, 4096, 12600, 65536, 1 << 18,
+                         1 << 20, 99991, 257, 1025, 53 * 8};
+    for (unsigned i = 0; i < sizeof sizes / sizeof sizes[0]; i++) run_c2c(sizes[i], sizes[i] > (1 << 17) ? 1 : 3);
+    const int rsizes[] = {2, 8, 64, 1000, 8192, 1 << 16, 1 << 22, 2 * 99991, 12600};
+    for (unsigned i = 0; i < sizeof rsizes / sizeof rsizes[0]; i++) run_real(rsizes[i], rsizes[i] > (1 << 20) ? 1 : 2);
+    run_conv(5, 3);
+    run_conv(300, 17);
+    run_conv(1000, 1000);
+    run_conv(1 << 16, 1000);
+
+    /* a caller edits the public fields between calls: the registry rebuilds its entry */
+    fft_object e = fft_init(64, 1);
+    fft_data *x = cbuf(64), *y = cbuf(64);
+    fft_exec(e, x, y);
+    e->sgn = -1;
+    for (int i = 0; i < 63; i++) e->twiddle[i].im = -e->twiddle[i].im;
+    fft_exec(e, x, y);
+    CHECK(hsfft_plan_refresh(e) == 0, "refresh");
+    fft_exec(e, x, y);
+    free_fft(e);
+    free(x);
+    free(y);
+    CHECK(hsfft_release_scratch() == 0, "release_scratch");
+
+    g_shared = fft_init(12600, 1);
+    pthread_t th[8];
+    for (long t = 0; t < 8; t++) pthread_create(&th[t], NULL, hammer, (void *)t);
+    for (int t = 0; t < 8; t++) pthread_join(th[t], NULL);
+    free_fft(g_shared);
+    CHECK(hsfft_release_scratch() == 0, "release_scratch 2");
+
+    if (fails) {
+        fprintf(stderr, "%d failures\n", fails);
+        return 1;
+    }
+    printf("sanitize: ok\n");
+    return 0;
+}

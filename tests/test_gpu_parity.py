@@ -286,6 +286,42 @@ def test_generic_odd_radices():
             assert T.bits_equal(gpu_c2c_batched(n, sgn, x), oracle_rows(x, sgn)), (n, sgn)
 
 
+@pytest.mark.parametrize("n", [64, 1000, 2 * 97])
+def test_real_and_convolve_batches_beyond_65535_rows(n):
+    """row helper kernels index rows by blockIdx.y (<= 65535 per launch): larger batches are
+    sliced; r2c (split not fused for these sizes), c2r and batched convolution of 70000 short
+    rows, sampled rows bit-exact vs the oracle"""
+    rows = 70000
+    x = T.real_input(n, 0xE0 ^ n, batch=rows).reshape(rows, n)
+    rp, ip = hsfft.RealPlan(n, 1), hsfft.RealPlan(n, -1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dX = hsfft.DeviceBuffer(rows * n * 16)
+    hsfft.r2c_batched(rp, din, dX, rows)
+    dY = hsfft.DeviceBuffer(rows * n * 8)
+    hsfft.c2r_batched(ip, dX, dY, rows)
+    hsfft.synchronize()
+    for r in (0, 65534, 65535, 65536, rows - 1):
+        X = dX.to_array(np.complex128, n, r * n * 16)
+        assert T.bits_equal(X, T.oracle_r2c(x[r], 1)), ("r2c", n, r)
+        y = dY.to_array(np.float64, n, r * n * 8)
+        assert T.bits_equal(y, T.oracle_c2r(X, n, -1)), ("c2r", n, r)
+    L = hsfft.lib()
+    m = 7
+    b = T.real_input(m, 0xE1 ^ n, batch=rows).reshape(rows, m)
+    db = hsfft.DeviceBuffer.from_array(b)
+    dout = hsfft.DeviceBuffer(rows * (n + m) * 8)
+    ln = L.hsfft_convolve_batched(b"full", b"linear", din.ptr, n, db.ptr, m, dout.ptr, rows)
+    assert ln == n + m - 1, L.hsfft_last_error()
+    for r in (0, 65535, rows - 1):
+        y = dout.to_array(np.float64, ln, r * ln * 8)
+        o = np.zeros(2 * (n + m) + 8)
+        assert T.oracle().orc_convolve(b"full", b"linear", T.ptr(np.ascontiguousarray(x[r])), n,
+                                       T.ptr(np.ascontiguousarray(b[r])), m, T.ptr(o), 0) == ln
+        assert T.bits_equal(y, o[:ln]), ("conv", n, r)
+    for d in (din, dX, dY, db, dout):
+        d.free()
+
+
 def test_batch_edge_cases():
     L = hsfft.lib()
     p = hsfft.Plan(64, 1)
@@ -376,13 +412,17 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
-def test_12600_row_kernel_variants(env, sgn, monkeypatch):
-    """config 3's schedules, bit-exact vs the oracle, both signs, a batch that leaves the
-    row-walking grid uneven (300 rows over 256 workgroups): mr::k_row2 with stages 0-1 fused
-    (default) and unfused, mr::k_row (one workgroup per row), the two mixed-radix passes."""
+@pytest.mark.parametrize("rows", [300, 64])
+def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
+    """config 3's schedules, bit-exact vs the oracle, both signs: 300 rows leave the
+    row-walking grid uneven (300 rows over 256 workgroups); 64 rows give every workgroup
+    exactly ONE row, so no row can lean on an earlier row's barriers (the stage-1 twiddles of
+    the fused first stages are read right after the per-workgroup LDS copy).  Variants:
+    mr::k_row2 with stages 0-1 fused (default) and unfused, mr::k_row (one workgroup per row),
+    the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    n, rows = 12600, 300
+    n = 12600
     x = T.complex_input(n, 77, batch=rows).reshape(rows, n)
     p = hsfft.Plan(n, sgn)
     assert p.num_passes() == (2 if env.get("HSFFT_MR_ROW") == "0" else 1)

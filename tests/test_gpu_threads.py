@@ -1,0 +1,150 @@
+"""Reentrancy of the drop-in API on the MI355X: several host threads call the reference's
+entry points at once (the reference's mixed-radix fft_exec is const on its plan and uses no
+globals, highSpeedFFT.c:1920-1942 / 318-1629; r2c/c2r/convolve malloc per call, real.c:87-88,
+convolve.c:104-154).  ctypes releases the GIL around every foreign call, so the threads below
+really are inside libhsfft together.
+
+Every output is compared BIT-EXACT with the oracle (CPU restatement pinned to the reference).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import hsfft_testlib as T
+
+import hsfft
+
+pytestmark = pytest.mark.gpu
+
+NTHREADS = 8
+ITERS = 6
+# ten distinct padded lengths P (2^7 .. 2^16): more than the 8 cached plan pairs, so cache
+# entries are evicted and rebuilt while other threads are still using theirs
+CONV = [(40 + 7 * k, (1 << (k + 6)) - 40 - 7 * k + 1) for k in range(10)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if hsfft.device_count() < 1:
+        pytest.skip("no GPU")
+    hsfft.lib().hsfft_set_device(0)
+    yield
+    hsfft.synchronize()
+
+
+def _conv_ref(a, b, typ=b"full"):
+    o = np.zeros(2 * (a.size + b.size) + 8)
+    ln = T.oracle().orc_convolve(typ, b"linear", T.ptr(a), a.size, T.ptr(b), b.size, T.ptr(o), 0)
+    return o[:ln].copy()
+
+
+def test_eight_threads_shared_plan_r2c_and_convolve():
+    L = hsfft.lib()
+    n_c = 12600                     # mixed radix 3/5/7/8 (config 3's length), ONE shared plan
+    shared = hsfft.Plan(n_c, 1)
+    n_r = 1 << 14                   # real path: one shared real plan
+    rplan = hsfft.RealPlan(n_r, 1)
+    n_b = 97                        # Bluestein: one plan per thread (the reference's rule)
+
+    xs = [T.complex_input(n_c, 0x7000 + t) for t in range(NTHREADS)]
+    ref_c = [T.oracle_c2c(x, 1) for x in xs]
+    rs = [T.real_input(n_r, 0x7100 + t) for t in range(NTHREADS)]
+    ref_r = [T.oracle_r2c(r, 1) for r in rs]
+    bs = [T.complex_input(n_b, 0x7200 + t) for t in range(NTHREADS)]
+    ref_b = [T.oracle_c2c(b, -1) for b in bs]
+    conv_in = []
+    for k, (n, m) in enumerate(CONV):
+        a, b = T.real_input(n, 0x7300 + k), T.real_input(m, 0x7400 + k)
+        conv_in.append((a, b, _conv_ref(a, b)))
+    assert len({1 << (n + m - 2).bit_length() for n, m in CONV}) >= 9
+
+    errors = []
+    start = threading.Barrier(NTHREADS)
+
+    def worker(t):
+        try:
+            L.hsfft_set_device(0)
+            bplan = hsfft.Plan(n_b, -1)
+            start.wait()
+            for it in range(ITERS):
+                y = np.zeros(n_c, dtype=np.complex128)
+                L.fft_exec(shared.ptr, T.ptr(xs[t]), T.ptr(y))
+                if not T.bits_equal(y, ref_c[t]):
+                    errors.append(("c2c", t, it, T.mismatches(y, ref_c[t])))
+                Y = np.zeros(n_r, dtype=np.complex128)
+                L.fft_r2c_exec(rplan.ptr, T.ptr(rs[t]), T.ptr(Y))
+                if not T.bits_equal(Y, ref_r[t]):
+                    errors.append(("r2c", t, it, T.mismatches(Y, ref_r[t])))
+                z = bplan.exec(bs[t])
+                if not T.bits_equal(z, ref_b[t]):
+                    errors.append(("bluestein", t, it))
+                k = (t * 3 + it) % len(CONV)
+                a, b, ref = conv_in[k]
+                o = np.zeros(ref.size + 8)
+                ln = L.fft_convolve(b"full", b"linear", T.ptr(a), a.size, T.ptr(b), b.size, T.ptr(o))
+                if ln != ref.size or not T.bits_equal(o[:ln], ref):
+                    errors.append(("convolve", t, it, k, ln))
+            bplan.close()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(("exception", t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(NTHREADS)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not any(x.is_alive() for x in th), "a worker thread did not finish"
+    assert not errors, errors[:10]
+
+
+def test_threads_batched_device_api_distinct_plans():
+    """the extension API from several threads: each thread its own device buffers, the
+    plans shared (2^20 two-pass, 4096, 12600 whole-row kernel), results bit-exact"""
+    sizes = [1 << 20, 4096, 12600, 1 << 16]
+    plans = {n: hsfft.Plan(n, 1) for n in sizes}
+    errors = []
+
+    def worker(t):
+        try:
+            hsfft.lib().hsfft_set_device(0)
+            n = sizes[t % len(sizes)]
+            rows = 2 if n == 1 << 20 else 5
+            x = T.complex_input(n, 0x7500 + t, batch=rows).reshape(rows, n)
+            din = hsfft.DeviceBuffer.from_array(x)
+            dout = hsfft.DeviceBuffer(x.nbytes)
+            for _ in range(3):
+                hsfft.exec_batched(plans[n], din, dout, rows)
+                hsfft.synchronize()
+                y = dout.to_array(np.complex128).reshape(rows, n)
+                if not T.bits_equal(y, T.oracle_c2c(x, 1)):
+                    errors.append((t, n))
+            din.free()
+            dout.free()
+        except Exception as e:  # pragma: no cover
+            errors.append(("exception", t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(NTHREADS)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not any(x.is_alive() for x in th)
+    assert not errors, errors
+
+
+def test_exec_multi_threads_single_device():
+    """hsfft_exec_multi runs one host thread per device (here ndev = 1: the shard thread
+    path and its error propagation)"""
+    import ctypes
+    n, rows = 4096, 6
+    x = T.complex_input(n, 0x7600, batch=rows).reshape(rows, n)
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    ins = (ctypes.c_void_p * 1)(din.ptr)
+    outs = (ctypes.c_void_p * 1)(dout.ptr)
+    assert hsfft.lib().hsfft_exec_multi(p.ptr, ins, outs, rows, 1) == 0
+    y = dout.to_array(np.complex128).reshape(rows, n)
+    assert T.bits_equal(y, T.oracle_c2c(x, 1))
+    assert hsfft.lib().hsfft_exec_multi(p.ptr, ins, outs, rows, 99) < 0   # more devices than exist
