@@ -486,6 +486,15 @@ def main():
         out["roofline"]["pass_ms"] = [round(p, 4) for p in pass_ms]
         out["roofline"]["pass_frac"] = [round(samples * bytes_per_sample / (p / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
                                         for p in pass_ms]
+    # (before the copy benchmark below overwrites dout)
+    if args.dump_rows and kind == "c2c":
+        import numpy as np
+        g0 = row_range(rank, batch)[0]
+        picks = sorted({0, batch - 1})
+        rows = np.stack([dout.to_array(np.complex128, n, r * n * 16) for r in picks])
+        os.makedirs(args.dump_rows, exist_ok=True)
+        np.savez(os.path.join(args.dump_rows, f"rank{rank}.npz"), rows=rows,
+                 global_rows=np.array([g0 + r for r in picks]), n=n, seed=seed, world=ws)
     # practical HBM ceiling on this device: a 16-B-per-lane stream copy of the same buffers
     nbytes = min(din.nbytes, dout.nbytes) // 16 * 16
     cms = hsfft.bench_copy(din, dout, nbytes, 5)
@@ -503,14 +512,6 @@ def main():
                                 "pcie_gbs": round(2 * hx.nbytes / hs / 1e9, 1),
                                 "note": "host (pageable numpy) rows in and out, upload/transform/download overlapped; "
                                         "PCIe-inclusive, not the headline value"}
-    if args.dump_rows and kind == "c2c":
-        import numpy as np
-        g0 = row_range(rank, batch)[0]
-        picks = sorted({0, batch - 1})
-        rows = np.stack([dout.to_array(np.complex128, n, r * n * 16) for r in picks])
-        os.makedirs(args.dump_rows, exist_ok=True)
-        np.savez(os.path.join(args.dump_rows, f"rank{rank}.npz"), rows=rows,
-                 global_rows=np.array([g0 + r for r in picks]), n=n, seed=seed, world=ws)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.c2r:
         out["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:

@@ -708,6 +708,25 @@ int hsd_host_register(void *p, size_t bytes)
     return 0;
 }
 
+/* page-locked host memory that kernels can read and write directly over the host link
+ * (the small-transform path of fft_exec) */
+void *hsd_host_alloc(size_t bytes)
+{
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_err(e, "hipHostMalloc");
+        return nullptr;
+    }
+    return p;
+}
+
+int hsd_host_free(void *p)
+{
+    if (p) HCHK(hipHostFree(p));
+    return 0;
+}
+
 int hsd_host_unregister(void *p)
 {
     HCHK(hipHostUnregister(p));

@@ -835,6 +835,32 @@ int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long lo
 }
 
 /* ------------------------------------------------------------------ drop-in fft_exec */
+/* Small host-pointer transforms (one pass, rows up to HSFFT_SMALL_KB, default 1 MiB): the
+ * rows are copied into page-locked host slots and the kernel reads and writes them over the
+ * host link directly -- no H2D / D2H copy launches, one kernel launch and one wait per call
+ * (BASELINE config 1, N = 1024).  Per-device slots, used under the device lock. */
+static void *g_pin[HS_MAX_DEV][2];
+static size_t g_pin_sz[HS_MAX_DEV];
+
+static int small_host_exec(hs_entry *e, const fft_data *inp, fft_data *oup, size_t bytes)
+{
+    const int d = hsd_get_device();
+    if (d < 0 || d >= HS_MAX_DEV) return 1;
+    if (g_pin_sz[d] < bytes) {
+        hsd_host_free(g_pin[d][0]);
+        hsd_host_free(g_pin[d][1]);
+        g_pin[d][0] = hsd_host_alloc(bytes);
+        g_pin[d][1] = hsd_host_alloc(bytes);
+        g_pin_sz[d] = g_pin[d][0] && g_pin[d][1] ? bytes : 0;
+        if (!g_pin_sz[d]) return 1; /* no pinned memory: the staged path */
+    }
+    memcpy(g_pin[d][0], inp, bytes);
+    int rc = hs_c2c_rows(e, g_pin[d][0], e->N, g_pin[d][1], e->N, 1);
+    if (!rc) rc = hsd_sync();
+    if (!rc) memcpy(oup, g_pin[d][1], bytes);
+    return rc;
+}
+
 static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
 {
     if (obj == NULL || inp == NULL || oup == NULL) {
@@ -853,8 +879,12 @@ static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
     const size_t bytes = sizeof(fft_data) * (size_t)N;
     const int din = hsd_is_device_ptr(inp), dout = hsd_is_device_ptr(oup);
     int rc;
+    const size_t small = (size_t)env_int("HSFFT_SMALL_KB", 1024) * 1024;
     if (din && dout && inp != oup) {
         rc = hs_c2c_rows(e, inp, N, oup, N, 1);
+    } else if (!din && !dout && e->lt == 0 && e->npass == 1 && bytes <= small &&
+               (rc = small_host_exec(e, inp, oup, bytes)) <= 0) {
+        /* done (rc 0) or failed (rc < 0) on the pinned path */
     } else {
         /* host (or aliased) buffers: staged through device memory, synchronous */
         fft_data *di = hs_scratch(5, bytes), *dq = hs_scratch(6, bytes);

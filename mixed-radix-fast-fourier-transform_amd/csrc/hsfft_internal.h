@@ -82,6 +82,8 @@ int hsd_d2h_async(void *h, const void *d, size_t bytes);
 int hsd_stream_sync(void);        /* the selected stream */
 int hsd_host_register(void *p, size_t bytes);
 int hsd_host_unregister(void *p);
+void *hsd_host_alloc(size_t bytes);  /* page-locked, device-accessible host memory */
+int hsd_host_free(void *p);
 int hsd_event_record(int i);      /* event ring (64 slots) on the selected stream */
 int hsd_event_wait(int i);
 void *hsd_stream(void);

@@ -59,6 +59,12 @@ int hsd_d2h_async(void *h, const void *d, size_t bytes) { return hsd_d2h(h, d, b
 int hsd_stream_sync(void) { return 0; }
 int hsd_host_register(void *p, size_t bytes) { return 0; }
 int hsd_host_unregister(void *p) { return 0; }
+void *hsd_host_alloc(size_t bytes) { return malloc(bytes ? bytes : 16); }
+int hsd_host_free(void *p)
+{
+    free(p);
+    return 0;
+}
 int hsd_event_record(int i) { return i < 0 ? -1 : 0; }
 int hsd_event_wait(int i) { return i < 0 ? -1 : 0; }
 void *hsd_stream(void) { return NULL; }
