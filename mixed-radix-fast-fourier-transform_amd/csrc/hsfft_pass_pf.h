@@ -65,6 +65,20 @@ __device__ __forceinline__ double2 ldg(const void *base, unsigned boff)
     return *(const double2 *)((const char *)base + boff);
 }
 __device__ __forceinline__ void stg(void *base, unsigned boff, double2 v) { *(double2 *)((char *)base + boff) = v; }
+/* non-temporal forms (streamed once: keep them from displacing cache-resident data) */
+typedef double pf_d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ldg_nt(const void *base, unsigned boff)
+{
+    const pf_d2v v = __builtin_nontemporal_load((const pf_d2v *)((const char *)base + boff));
+    return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void stg_nt(void *base, unsigned boff, double2 v)
+{
+    pf_d2v u;
+    u.x = v.x;
+    u.y = v.y;
+    __builtin_nontemporal_store(u, (pf_d2v *)((char *)base + boff));
+}
 
 /* ------------------------------------------------------------------ first pass
  * [R0, 8^N8] leaf pass (B == 1): input [t][m] (t < P, m < A), output [m][u].  A workgroup
@@ -275,7 +289,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
  * twiddles (k = q + B*kloc) are row-independent: stages 0/1 as LDS runs, stage 2 in
  * registers.  Row prefetch (PREF) is opt-in: it costs the VGPRs that make the kernel spill. */
 /* stages + exchanges + store of one [8,8,8] tile-row; ocol = output row + q */
-template <int SGN>
+template <int SGN, bool NTS = false>
 __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], const double2 (&w2)[7], double2 *lds,
                                           const double2 *ltw, double2 *orow, unsigned B, unsigned lane, unsigned jt,
                                           unsigned g)
@@ -292,7 +306,10 @@ __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], cons
     r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
     stage<8, SGN>(xr, xi, w2, false);
 #pragma unroll
-    for (int jj = 0; jj < 8; jj++) stg(orow + (size_t)jj * TPG * B, lane, make_double2(xr[jj], xi[jj]));
+    for (int jj = 0; jj < 8; jj++) {
+        if constexpr (NTS) stg_nt(orow + (size_t)jj * TPG * B, lane, make_double2(xr[jj], xi[jj]));
+        else stg(orow + (size_t)jj * TPG * B, lane, make_double2(xr[jj], xi[jj]));
+    }
 }
 
 template <int T, int SGN, bool CONJ, bool PREF = true>
@@ -675,6 +692,8 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         snprintf(g_err, sizeof g_err, "pf: bad grid %lld", grid);
         return -1;
     }
+    /* dev probe: HSFFT_PF_OCC1=1 pads the dynamic LDS so only one workgroup fits per CU */
+    if (env("HSFFT_PF_OCC1", 0)) lds = lds > 100 * 1024 ? lds : 100 * 1024;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return set_err(e, "hipFuncSetAttribute");
