@@ -278,6 +278,63 @@ def bench_c1(args, comm, ws, rank):
     dx.free()
 
 
+def other_configs(steps=3, warmup=1):
+    """The other BASELINE configs, each at its full per-GPU workload, timed in the same run
+    as the headline (one rank): wall time over `steps` steps between device synchronisations,
+    inputs generated in HBM.  c1 is the median latency of single host-buffer fft_exec calls."""
+    import numpy as np
+    out = {}
+    L = hsfft.lib()
+    # c1: one N=1024 transform on host buffers
+    p1 = hsfft.Plan(1024, 1)
+    x = np.ascontiguousarray(np.exp(1j * np.arange(1024.0)))
+    y = np.zeros_like(x)
+    px, py = x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p)
+    for _ in range(20):
+        L.fft_exec(p1.ptr, px, py)
+    lat = []
+    for _ in range(300):
+        t = time.perf_counter()
+        L.fft_exec(p1.ptr, px, py)
+        lat.append(time.perf_counter() - t)
+    lat.sort()
+    out["c1"] = {"value": round(lat[len(lat) // 2] * 1e6, 2), "unit": "us", "workload": CONFIGS["c1"][4]}
+    p1.close()
+    for name in ("c3", "c4", "c5"):
+        kind, n, batch, seed, desc = CONFIGS[name]
+        if kind == "c2c":
+            plan = hsfft.Plan(n, 1)
+            din, dout = hsfft.DeviceBuffer(n * batch * 16), hsfft.DeviceBuffer(n * batch * 16)
+            hsfft.fill_complex(din, n * batch, seed, 0)
+            run = lambda: hsfft.exec_batched(plan, din, dout, batch)  # noqa: E731
+        else:
+            plan = hsfft.RealPlan(n, 1)
+            chunk = min(batch, max(1, (64 << 30) // (n * 16)))
+            din, dout = hsfft.DeviceBuffer(n * batch * 8), hsfft.DeviceBuffer(chunk * n * 16)
+            hsfft.fill_real(din, n * batch, seed, 0)
+
+            def run():
+                for c0 in range(0, batch, chunk):
+                    hsfft.check(L.hsfft_r2c_batched(plan.ptr, ctypes.c_void_p(din.ptr + c0 * n * 8),
+                                                    ctypes.c_void_p(dout.ptr), min(chunk, batch - c0)), "r2c")
+        for _ in range(warmup):
+            run()
+        hsfft.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        hsfft.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        bps = 32 if kind == "c2c" else 24
+        out[name] = {"value": round(n * batch / (ms / 1e3) / 1e9, 3), "unit": "GSamples/s", "ms_per_step": round(ms, 3),
+                     "steps": steps, "frac": round(n * batch * bps / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "workload": desc}
+        din.free()
+        dout.free()
+        plan.close()
+    return out
+
+
 def bench_convolve(args, comm, ws, rank):
     """batched linear convolution: r2c (compact, split fused) x2, spectral product on bins
     0..P/2, c2r, scale, 'full' window copy -- the GPU form of convolve.c:74-214"""
@@ -329,6 +386,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch (development only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="c2, one rank: skip timing BASELINE configs c1, c3, c4, c5 after the headline")
     ap.add_argument("--r2c-compact", action="store_true",
                     help="c5 only: hsfft_r2c_batched_compact (N/2+1 bins per row) instead of the reference layout")
     ap.add_argument("--c2r", action="store_true",
@@ -514,6 +573,10 @@ def main():
                                         "PCIe-inclusive, not the headline value"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.c2r:
         out["cpu_baseline"] = cpu_baseline(cfg)
+    if ws == 1 and args.config == "c2" and not args.batch and not args.no_other_configs:
+        din.free()
+        dout.free()
+        out["other_configs"] = other_configs()
     if rank == 0:
         print(json.dumps(out), flush=True)
     din.free()

@@ -14,7 +14,7 @@ for spec in "$@"; do
   i=$((i+1))
   envs=$(echo "$spec" | cut -d'|' -f1); bargs=$(echo "$spec" | cut -s -d'|' -f2)
   echo "=== [$i] env: $envs args: ${bargs:-default}"
-  env $(echo "$envs" | tr ';' ' ') timeout -k 10 300 python bench.py ${CPU_BASE:---no-cpu-baseline} ${bargs:---steps 5 --warmup 2} > gpurun_out/bench_$i.log 2>&1
+  env $(echo "$envs" | tr ';' ' ') timeout -k 10 300 python bench.py ${CPU_BASE:---no-cpu-baseline --no-other-configs} ${bargs:---steps 5 --warmup 2} > gpurun_out/bench_$i.log 2>&1
   rc=$?; echo "rc=$rc"; python3 -c "
 import json,sys
 for l in open('gpurun_out/bench_$i.log'):
