@@ -80,13 +80,15 @@ __device__ __forceinline__ void runs_to_lds(double2 *ltw, const double2 *tw, uns
  * t < 256 (i < 4 of a thread's 8 points t = jt + 64 i) can hold input: the other four are
  * the reference's zero padding (exact +0.0, fed through the same butterfly).  The chirp
  * values of the thread's points are row-invariant and stay in registers for all T rows. */
-template <int T, int S>
-__global__ __launch_bounds__(512, 4) void k_bfirst(Args a)
+/* SPLIT: exchanges through a 32 KiB image (real parts, then imaginary parts), so that three
+ * workgroups fit per CU (LDS 40 KiB, launch bound 6 waves per SIMD: <= 80 VGPRs) */
+template <int T, int S, bool SPLIT = false>
+__global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_bfirst(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
     constexpr unsigned A = 512;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    double2 *ltw = lds + P * G; /* tw[0, 511): stages L = 8 (kloc < 8) and 64 */
+    double2 *ltw = lds + (SPLIT ? P * G / 2 : P * G); /* tw[0, 511): stages L = 8 (kloc < 8) and 64 */
     unsigned bg, tile;
     split_block(a, bg, tile);
     const unsigned tid0 = threadIdx.x;
@@ -128,11 +130,11 @@ __global__ __launch_bounds__(512, 4) void k_bfirst(Args a)
         }
         double2 w[7];
         pf::stage<8, S>(xr, xi, w, true);
-        r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+        r8::exchange<8, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
 #pragma unroll
         for (int i = 0; i < 7; i++) w[i] = ltw[7 + 7 * (jt & 7) + i];
         pf::stage<8, S>(xr, xi, w, false);
-        r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+        r8::exchange<8, 8, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
 #pragma unroll
         for (int i = 0; i < 7; i++) w[i] = ltw[63 + 7 * (jt & 63) + i];
         pf::stage<8, S>(xr, xi, w, false);
@@ -216,13 +218,13 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
 /* Inverse FFT's second pass [8,8,8] at L = B = 512 (sign -S, conjugated twiddles) of q-tile
  * q0 for T rows, stored through the chirp for n < nsig (direction S).  Row prefetch (PREF)
  * is opt-in (HSFFT_BLUE_PREF=1), as for pf::k_b512: with it the kernel spills 20 B. */
-template <int T, int S, bool PREF = true>
-__global__ __launch_bounds__(512, 4) void k_blast(Args a)
+template <int T, int S, bool PREF = true, bool SPLIT = false>
+__global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
     constexpr unsigned B = 512;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    double2 *ltw = lds + P * G;
+    double2 *ltw = lds + (SPLIT ? P * G / 2 : P * G);
     unsigned bg, tile;
     split_block(a, bg, tile);
     const unsigned tid0 = threadIdx.x, q0 = tile * G;
@@ -241,9 +243,16 @@ __global__ __launch_bounds__(512, 4) void k_blast(Args a)
         }
     }
     double2 w2[7];
-    r8::load_tw_co<64>(w2, a, tid0 / G, q0);
-    runs_to_lds<true>(ltw, a.tw, B, q0, tid0);
-    r8::redistribute_tw(w2, lds);
+    if constexpr (SPLIT) { /* per-lane run (the redistribution image would not fit) */
+        const long long base = 64LL * B - 1 + 7LL * (q0 + tid0 % G + (long long)B * (tid0 / G));
+#pragma unroll
+        for (int i = 0; i < 7; i++) w2[i] = a.tw[base + i];
+        runs_to_lds<true>(ltw, a.tw, B, q0, tid0);
+    } else {
+        r8::load_tw_co<64>(w2, a, tid0 / G, q0);
+        runs_to_lds<true>(ltw, a.tw, B, q0, tid0);
+        r8::redistribute_tw(w2, lds);
+    }
 #pragma unroll
     for (int i = 0; i < 7; i++) w2[i].y = -w2[i].y;
     __syncthreads();
@@ -287,11 +296,11 @@ __global__ __launch_bounds__(512, 4) void k_blast(Args a)
 #pragma unroll
         for (int i = 0; i < 7; i++) w[i] = ltw[7 * g + i];
         pf::stage<8, -S>(xr, xi, w, false);
-        r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+        r8::exchange<8, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
 #pragma unroll
         for (int i = 0; i < 7; i++) w[i] = ltw[56 * (1 + (jt & 7)) + 7 * g + i];
         pf::stage<8, -S>(xr, xi, w, false);
-        r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+        r8::exchange<8, 8, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
         pf::stage<8, -S>(xr, xi, w2, false);
         /* output n = u*B + q, u = jt + 64 jj; only n < nsig is stored (ref :1871-1886) */
         double2 *orow = a.out + (long long)(b0 + it) * a.odist;
@@ -321,7 +330,14 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     const int t = env("HSFFT_BLUE_T", 8); /* measured c4: T 2 17.8, 4 18.7, 8 19.1 GS/s */
     const int T = t >= 8 ? 8 : t >= 4 ? 4 : t >= 2 ? 2 : 1;
     kfn fn;
-    if (which == 2)
+    /* HSFFT_BLUE_SPLIT bit 0: k_bfirst, bit 1: k_blast with the split exchange (3 per CU) */
+    const int split = env("HSFFT_BLUE_SPLIT", 0);
+    const bool sp = (which == 2 && (split & 1)) || (which == 1 && (split & 2));
+    if (which == 2 && sp && T == 8)
+        fn = sgn == 1 ? k_bfirst<8, 1, true> : k_bfirst<8, -1, true>;
+    else if (which == 1 && sp && T == 8)
+        fn = sgn == 1 ? k_blast<8, 1, false, true> : k_blast<8, -1, false, true>;
+    else if (which == 2)
         fn = sgn == 1 ? (T == 8 ? k_bfirst<8, 1> : T == 4 ? k_bfirst<4, 1> : T == 2 ? k_bfirst<2, 1> : k_bfirst<1, 1>)
                       : (T == 8 ? k_bfirst<8, -1> : T == 4 ? k_bfirst<4, -1> : T == 2 ? k_bfirst<2, -1> : k_bfirst<1, -1>);
     else if (which == 0)
@@ -350,7 +366,7 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     const long long grid = a.tiles * ((batch + T - 1) / T);
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     /* image + twiddle runs (k_bfirst: 511; k_bmid: 504 forward runs + 511 inverse entries) */
-    const size_t lds = (size_t)(512 * 8 + (which == 0 ? 1016 : 512)) * sizeof(double2);
+    const size_t lds = (size_t)((sp && T == 8 ? 512 * 4 : 512 * 8) + (which == 0 ? 1016 : 512)) * sizeof(double2);
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a);
     HCHK(hipGetLastError());

@@ -37,7 +37,18 @@ struct MArgs {
     int A, B, tiles_q, tiles, batch;
     int sgn, conj;
     int xcd; /* XCD-aware block remap */
+    unsigned *dbg; /* k_row2 phase trace (HSFFT_ROW_DEBUG): 8 cumulative phase times per workgroup */
 };
+
+/* phase clock of the k_row2 trace: thread 0 adds the 100 MHz ticks since the last mark */
+__device__ __forceinline__ void mark(const MArgs &a, unsigned &tp, int slot)
+{
+    if (a.dbg && threadIdx.x == 0) {
+        const unsigned t = (unsigned)__builtin_amdgcn_s_memrealtime();
+        a.dbg[blockIdx.x * 8 + slot] += t - tp;
+        tp = t;
+    }
+}
 
 constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 
@@ -435,6 +446,7 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     /* fused01 reads the stage-1 entries before the first exchange's barrier, so the copy
      * needs a barrier of its own (once per workgroup) */
     __syncthreads();
+    unsigned tp = (unsigned)__builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
     for (unsigned b = blockIdx.x; b < (unsigned)a.batch; b += gridDim.x) {
         int jt = jt0;
@@ -444,8 +456,13 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         double xr[NM], xi[NM];
         if constexpr (F01) {
             fused01<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, ldsd, jt, sgn);
+            if (a.dbg) {
+                r8::pin(*reinterpret_cast<double(*)[8]>(xr));
+                mark(a, tp, 0); /* loads + stages 0-1 */
+            }
             xchg1_f01<R0, R1, R2, P, TPG>(xr, ldsd, jt);
             xchg1_f01<R0, R1, R2, P, TPG>(xi, ldsd, jt);
+            mark(a, tp, 1);
         } else {
             {
                 constexpr int NBF = P / R0, NB = cdiv(NBF, TPG);
@@ -468,11 +485,18 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         }
         rstage<R2, LS::Lloc(2), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
         xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, ldsd, jt);
+        mark(a, tp, 2);
         rstage<R3, LS::Lloc(3), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
         xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, ldsd, jt);
+        mark(a, tp, 3);
         rstage<R4, LS::Lloc(4), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(4) - 1), jt, sgn);
         xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, ldsd, jt);
+        mark(a, tp, 4);
         rstage<R5, LS::Lloc(5), P, TPG, false, CONJ>(xr, xi, a.tw + (LS::Lloc(5) - 1), jt, sgn);
+        if (a.dbg) {
+            r8::pin(*reinterpret_cast<double(*)[8]>(xr));
+            mark(a, tp, 5); /* last stage (global twiddles) */
+        }
         constexpr int LL = LS::Lloc(5), NBFL = P / R5, NBL = cdiv(NBFL, TPG);
 #pragma unroll
         for (int c = 0; c < NBL; c++) {
@@ -482,6 +506,8 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             for (int jj = 0; jj < R5; jj++)
                 pf::stg(out, (unsigned)(kloc + jj * LL) * 16u, make_double2(xr[c * R5 + jj], xi[c * R5 + jj]));
         }
+        mark(a, tp, 6); /* stores issued */
+        if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + 7] += 1;
     }
 }
 
@@ -560,6 +586,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         return -4;
     }
     MArgs a;
+    memset(&a, 0, sizeof a);
     a.in = (const double2 *)l->in;
     a.out = (double2 *)l->out;
     a.tw = (const double2 *)l->tw;
@@ -591,9 +618,28 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         const int grid = l->batch < ncu ? l->batch : (ncu > 0 ? ncu : 256);
         a.tiles = a.tiles_q = 1;
+        static unsigned *s_dbg = nullptr;
+        const char *de = getenv("HSFFT_ROW_DEBUG");
+        if (de && atoi(de) && grid <= 4096) {
+            if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, 4096 * 8 * sizeof(unsigned)));
+            HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 8 * sizeof(unsigned), st));
+            a.dbg = s_dbg;
+        }
         HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(1024), lds, st, a);
         HCHK(hipGetLastError());
+        if (a.dbg) {
+            static unsigned h[4096 * 8];
+            HCHK(hipStreamSynchronize(st));
+            HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
+            double ph[8] = {0};
+            for (int g = 0; g < grid; g++)
+                for (int k = 0; k < 8; k++) ph[k] += h[g * 8 + k];
+            const double rows = ph[7] > 0 ? ph[7] : 1;
+            fprintf(stderr, "k_row2 per row (us): load+st01 %.2f x01 %.2f st2+x %.2f st3+x %.2f st4+x %.2f st5 %.2f store %.2f | rows %.0f\n",
+                    ph[0] / rows / 100, ph[1] / rows / 100, ph[2] / rows / 100, ph[3] / rows / 100, ph[4] / rows / 100,
+                    ph[5] / rows / 100, ph[6] / rows / 100, rows);
+        }
         return 0;
     }
     if (v->row) {
