@@ -417,6 +417,7 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
  * Saves the c2c output's write and re-read (16 of 56 bytes per real sample). */
 /* one tile's row loads, its stage-0/1 twiddle runs (-> ltw) and stage-2 twiddles (coalesced,
  * redistributed through the image: every earlier reader of the image must be done) */
+template <int PROBE = 0>
 __device__ __forceinline__ void r2c_load(double (&xr)[8], double (&xi)[8], double2 (&w2)[7], const double2 *row,
                                          unsigned B, unsigned q0, const double2 *tw, double2 *lds, double2 *ltw,
                                          unsigned tid0)
@@ -432,14 +433,19 @@ __device__ __forceinline__ void r2c_load(double (&xr)[8], double (&xi)[8], doubl
     r8::Args ta;
     ta.tw = tw;
     ta.B = B;
-    r8::load_tw_co<64>(w2, ta, (int)(tid0 >> 3), q0);
+    if constexpr (PROBE & 2) { /* timing probe: no stage-2 twiddle loads (wrong results) */
+#pragma unroll
+        for (int i = 0; i < 7; i++) w2[i] = make_double2(1.0, 0.0);
+    } else {
+        r8::load_tw_co<64>(w2, ta, (int)(tid0 >> 3), q0);
+    }
     __syncthreads(); /* earlier readers of the image and of ltw are done */
     if (tid0 < 504) {
         const unsigned r = tid0 / 56, e = tid0 % 56;
         const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
         ltw[tid0] = tw[src];
     }
-    r8::redistribute_tw(w2, lds);
+    if constexpr (!(PROBE & 2)) r8::redistribute_tw(w2, lds);
     __syncthreads(); /* ltw written; every wave has read its redistributed twiddles back */
 }
 
@@ -464,7 +470,9 @@ __device__ __forceinline__ void r2c_stages(double (&xr)[8], double (&xi)[8], con
     stage<8, SGN>(xr, xi, w2, false);
 }
 
-template <int SGN, bool COMPACT>
+/* PROBE (timing only, HSFFT_R2C_PROBE; results WRONG): bit 0 twiddle2 not loaded, bit 1
+ * stage-2 twiddles not loaded -- what the twiddle traffic costs */
+template <int SGN, bool COMPACT, int PROBE = 0>
 __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -483,9 +491,9 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
     if (j < tiles - 1) {
         const unsigned qlo = 8 * j + 1, qhi = B - 8 * j - 8;
         double hr[8], hi[8];
-        r2c_load(hr, hi, w2, row, B, qhi, a.tw, lds, ltw, tid0);
+        r2c_load<PROBE>(hr, hi, w2, row, B, qhi, a.tw, lds, ltw, tid0);
         r2c_stages<SGN, false>(hr, hi, w2, lds, ltw, tid0);
-        r2c_load(xr, xi, w2, row, B, qlo, a.tw, lds, ltw, tid0);
+        r2c_load<PROBE>(xr, xi, w2, row, B, qlo, a.tw, lds, ltw, tid0);
         /* the hi tile's real parts wait in the image's upper half (the lo tile's split
          * exchanges use the lower half), so only its imaginary parts stay in registers */
 #pragma unroll
@@ -502,15 +510,15 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
             const unsigned s = (P - 1 - u) * G + (7 - g);
             const double2 zk = make_double2(xr[jj], xi[jj]), zh = make_double2(ld[4096 + s], ld[s]);
             double re, im;
-            r8::r2c_pair(zk, zh, w2t[k], re, im);
+            r8::r2c_pair(zk, zh, (PROBE & 1) ? make_double2(1.0, 0.0) : w2t[k], re, im);
             X[k] = make_double2(re, im);
             if (!COMPACT) X[N - k] = make_double2(re, -im);
-            r8::r2c_pair(zh, zk, w2t[hk], re, im);
+            r8::r2c_pair(zh, zk, (PROBE & 1) ? make_double2(1.0, 0.0) : w2t[hk], re, im);
             X[hk] = make_double2(re, im);
             if (!COMPACT) X[N - hk] = make_double2(re, -im);
         }
     } else { /* column 0: k = u*B pairs with (P-u)*B */
-        r2c_load(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
+        r2c_load<PROBE>(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
         r2c_stages<SGN, false>(xr, xi, w2, lds, ltw, tid0);
         __syncthreads();
 #pragma unroll
@@ -557,6 +565,13 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     const size_t lds = (size_t)(512 * 8 + 504) * sizeof(double2);
     void (*fn)(Args, unsigned) = compact ? (sgn == 1 ? k_r2c_fused<1, true> : k_r2c_fused<-1, true>)
                                          : (sgn == 1 ? k_r2c_fused<1, false> : k_r2c_fused<-1, false>);
+    {
+        const char *pe = getenv("HSFFT_R2C_PROBE");
+        const int pr = pe ? atoi(pe) & 3 : 0;
+        if (pr == 1 && sgn == 1 && !compact) fn = k_r2c_fused<1, false, 1>;
+        if (pr == 2 && sgn == 1 && !compact) fn = k_r2c_fused<1, false, 2>;
+        if (pr == 3 && sgn == 1 && !compact) fn = k_r2c_fused<1, false, 3>;
+    }
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a, (unsigned)h);
     HCHK(hipGetLastError());
