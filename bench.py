@@ -385,6 +385,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch (development only)")
+    ap.add_argument("--n", type=int, default=0, help="override the transform length (development only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="c2, one rank: skip timing BASELINE configs c1, c3, c4, c5 after the headline")
@@ -431,6 +432,9 @@ def main():
         desc += " [compact N/2+1 output, hsfft_r2c_batched_compact]"
     if args.c2r and kind == "r2c":
         desc = desc.replace("r2c", "c2r", 1) + " [hsfft_c2r_batched, N/2+1 bins read per row]"
+    if args.n:
+        desc += f" [N overridden to {args.n}: not the BASELINE workload]"
+        n = args.n
     if args.batch:
         desc += f" [per-GPU batch overridden to {args.batch}: not the BASELINE workload]"
         batch = args.batch
@@ -573,7 +577,7 @@ def main():
                                         "PCIe-inclusive, not the headline value"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.c2r:
         out["cpu_baseline"] = cpu_baseline(cfg)
-    if ws == 1 and args.config == "c2" and not args.batch and not args.no_other_configs:
+    if ws == 1 and args.config == "c2" and not args.batch and not args.n and not args.no_other_configs:
         din.free()
         dout.free()
         out["other_configs"] = other_configs()

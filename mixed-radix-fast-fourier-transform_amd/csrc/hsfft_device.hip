@@ -205,7 +205,84 @@ __device__ void stage_odd(const KArgs &a, const double2 *src, double2 *dst, int 
     }
 }
 
-template <bool ODD>
+/* the same stage for a compile-time odd radix R (11..53): fully unrolled, so every value
+ * lives in registers (stage_odd's runtime-sized arrays live in scratch memory).  The
+ * butterfly is hsb::bfly_odd's arithmetic in the same order (ref :1475-1628): the symmetric
+ * sums / differences overwrite the inputs in place, and each output pair is written to the
+ * LDS image as soon as it is formed, so no output array is held. */
+template <int R>
+__device__ void stage_oddT(const KArgs &a, const double2 *src, double2 *dst, int Lloc, const double *cs,
+                           long long m0, long long q0)
+{
+    constexpr int MID = (R - 1) / 2;
+    const double *sn = cs + (R - 1);
+    const int P = a.P, G = a.G;
+    const int S = P / (Lloc * R);
+    const int nb = (P / R) * G;
+    const long long L = a.B * Lloc;
+    const double sg = (double)a.sgn;
+    for (int bf = threadIdx.x; bf < nb; bf += blockDim.x) {
+        const int gi = bf % G, j = bf / G;
+        const int kloc = j % Lloc, ml = j / Lloc;
+        double xr[R], xi[R];
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            double2 v = src[((ml + i * S) * Lloc + kloc) * G + gi];
+            xr[i] = v.x;
+            xi[i] = v.y;
+        }
+        const long long q = q0 + gi % a.Wq, m = m0 + gi / a.Wq;
+        if (q < a.B && m < a.A) { /* odd radices multiply every column, k = 0 included (:1552-1560) */
+            const long long k = q + a.B * kloc;
+            const double2 *w = a.tw + (L - 1 + (long long)(R - 1) * k);
+#pragma unroll
+            for (int i = 1; i < R; i++) {
+                double2 t = w[i - 1];
+                hsb::twmul(xr[i], xi[i], t.x, a.conj ? -t.y : t.y);
+            }
+        }
+        /* tr[i] -> xr[i+1], tr[i+MID] -> xr[R-1-i] (likewise ti) */
+#pragma unroll
+        for (int i = 0; i < MID; i++) {
+            const double ar = xr[i + 1], br = xr[R - 1 - i], ai = xi[i + 1], bi = xi[R - 1 - i];
+            xr[i + 1] = ar + br;
+            xi[R - 1 - i] = ai - bi;
+            xi[i + 1] = ai + bi;
+            xr[R - 1 - i] = ar - br;
+        }
+        double2 *out = dst + (ml * Lloc * R + kloc) * G + gi;
+        {
+            double ar = xr[0], ai = xi[0];
+#pragma unroll
+            for (int i = 0; i < MID; i++) {
+                ar += xr[i + 1];
+                ai += xi[i + 1];
+            }
+            out[0] = make_double2(ar, ai);
+        }
+#pragma unroll
+        for (int u = 0; u < MID; u++) {
+            double ur = xr[0], ui = xi[0], vr = 0.0, vi = 0.0;
+#pragma unroll
+            for (int v = 0; v < MID; v++) {
+                const int t = ((u + 1) * (v + 1)) % R - 1;
+                const double c = cs[t], d = sn[t];
+                ur += c * xr[v + 1];
+                ui += c * xi[v + 1];
+                vr -= d * xr[R - 1 - v];
+                vi -= d * xi[R - 1 - v];
+            }
+            vr = sg * vr;
+            vi = sg * vi;
+            out[(u + 1) * Lloc * G] = make_double2(ur - vi, ui + vr);
+            out[(R - u - 1) * Lloc * G] = make_double2(ur + vi, ui - vr);
+        }
+    }
+}
+
+/* OR: 0 = no odd radix in the pass, > 0 = the pass's only odd radix (compile-time stage,
+ * registers sized for that radix), -1 = several odd radices (runtime stage_odd) */
+template <int OR>
 __global__ __launch_bounds__(256) void k_pass_generic(KArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -238,7 +315,8 @@ __global__ __launch_bounds__(256) void k_pass_generic(KArgs a)
         case 7: stage_fixed<7>(a, src, dst, Lloc, leaf, m0, q0); break;
         case 8: stage_fixed<8>(a, src, dst, Lloc, leaf, m0, q0); break;
         default:
-            if constexpr (ODD) stage_odd(a, src, dst, r, Lloc, a.gcs + a.gcs_off[s], m0, q0);
+            if constexpr (OR > 0) stage_oddT<OR>(a, src, dst, Lloc, a.gcs + a.gcs_off[s], m0, q0);
+            else if constexpr (OR < 0) stage_odd(a, src, dst, r, Lloc, a.gcs + a.gcs_off[s], m0, q0);
             break;
         }
         __syncthreads();
@@ -917,13 +995,32 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
         snprintf(g_err, sizeof g_err, "hsd_run_pass: bad launch geometry (grid %lld, lds %zu)", grid, lds);
         return -1;
     }
-    bool odd = false;
+    int oddr = 0; /* the pass's odd radix (>= 11), -1 if it has two different ones */
     for (int s = 0; s < p->nst; s++) {
         const int r = p->radix[s];
-        odd |= !(r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8);
+        if (r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8) continue;
+        oddr = oddr == 0 || oddr == r ? r : -1;
     }
-    if (odd) hipLaunchKernelGGL(k_pass_generic<true>, dim3((unsigned)grid), dim3(256), lds, stream(), a);
-    else hipLaunchKernelGGL(k_pass_generic<false>, dim3((unsigned)grid), dim3(256), lds, stream(), a);
+    if (getenv("HSFFT_ODD_RUNTIME") && oddr > 0) oddr = -1; /* dev: the runtime-radix stage */
+    typedef void (*gfn)(KArgs);
+    gfn fn;
+    switch (oddr) { /* every odd radix the reference planner produces (factors(): 11..53) */
+    case 0: fn = k_pass_generic<0>; break;
+    case 11: fn = k_pass_generic<11>; break;
+    case 13: fn = k_pass_generic<13>; break;
+    case 17: fn = k_pass_generic<17>; break;
+    case 19: fn = k_pass_generic<19>; break;
+    case 23: fn = k_pass_generic<23>; break;
+    case 29: fn = k_pass_generic<29>; break;
+    case 31: fn = k_pass_generic<31>; break;
+    case 37: fn = k_pass_generic<37>; break;
+    case 41: fn = k_pass_generic<41>; break;
+    case 43: fn = k_pass_generic<43>; break;
+    case 47: fn = k_pass_generic<47>; break;
+    case 53: fn = k_pass_generic<53>; break;
+    default: fn = k_pass_generic<-1>; break;
+    }
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(256), lds, stream(), a);
     HCHK(hipGetLastError());
     return 0;
 }

@@ -279,9 +279,17 @@ def test_divergences_d3_d5_d6():
             assert np.abs(y - X).max() <= 1e-10 * max(1.0, np.abs(X).max()), n
 
 
-def test_generic_odd_radices():
-    for n in [11, 121, 17 * 8, 23 * 4, 29 * 3, 31, 37 * 5, 41, 43 * 2, 47, 53 * 8]:
-        x = T.complex_input(n, 3, batch=2).reshape(2, n)
+@pytest.mark.parametrize("runtime", ["0", "1"])
+def test_generic_odd_radices(runtime, monkeypatch):
+    """radices 11..53 (ref :1475-1628): one compile-time kernel per odd radix (registers, no
+    scratch), passes holding two different odd radices (11*13*8, 17*19, 29*31) on the
+    runtime-radix stage; HSFFT_ODD_RUNTIME=1 forces the runtime stage everywhere"""
+    if runtime == "1":
+        monkeypatch.setenv("HSFFT_ODD_RUNTIME", "1")
+    for n in [11, 121, 17 * 8, 23 * 4, 29 * 3, 31, 37 * 5, 41, 43 * 2, 47, 53 * 8, 11 * 13 * 8, 17 * 19, 29 * 31,
+              11 ** 4, 53 * 4096]:
+        rows = 2 if n < 100000 else 1
+        x = T.complex_input(n, 3, batch=rows).reshape(rows, n)
         for sgn in (1, -1):
             assert T.bits_equal(gpu_c2c_batched(n, sgn, x), oracle_rows(x, sgn)), (n, sgn)
 
