@@ -642,6 +642,26 @@ int hsd_sync(void)
     return fz_check();
 }
 
+/* wait for the library stream by polling an event (no blocking wait / wake-up): for short
+ * synchronous calls (the small host-buffer fft_exec) */
+int hsd_sync_spin(void)
+{
+    static thread_local hipEvent_t ev[HS_MAX_DEV];
+    static thread_local bool have[HS_MAX_DEV];
+    const int dev = cur_dev();
+    if (!have[dev]) {
+        HCHK(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
+        have[dev] = true;
+    }
+    HCHK(hipEventRecord(ev[dev], primary()));
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev[dev]);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return set_err(e, "hipEventQuery");
+    }
+    return fz_check();
+}
+
 int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
                 int conj, int rows_per_group, int lag, int grid)
 {

@@ -864,7 +864,7 @@ static int small_host_exec(hs_entry *e, const fft_data *inp, fft_data *oup, size
     }
     memcpy(g_pin[d][0], inp, bytes);
     int rc = hs_c2c_rows(e, g_pin[d][0], e->N, g_pin[d][1], e->N, 1);
-    if (!rc) rc = hsd_sync();
+    if (!rc) rc = env_int("HSFFT_SMALL_SPIN", 0) ? hsd_sync_spin() : hsd_sync();
     if (!rc) memcpy(oup, g_pin[d][1], bytes);
     return rc;
 }

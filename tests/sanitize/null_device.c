@@ -49,6 +49,7 @@ int hsd_memset_async(void *d, int v, size_t bytes)
     return 0;
 }
 int hsd_sync(void) { return 0; }
+int hsd_sync_spin(void) { return 0; }
 int hsd_select_stream(int idx)
 {
     sidx = idx;
