@@ -218,7 +218,8 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
 /* Inverse FFT's second pass [8,8,8] at L = B = 512 (sign -S, conjugated twiddles) of q-tile
  * q0 for T rows, stored through the chirp for n < nsig (direction S).  Row prefetch (PREF)
  * is opt-in (HSFFT_BLUE_PREF=1), as for pf::k_b512: with it the kernel spills 20 B. */
-template <int T, int S, bool PREF = true, bool SPLIT = false>
+/* PROBE (timing only, HSFFT_BLUE_PROBE=1; results WRONG): no chirp loads in the store loop */
+template <int T, int S, bool PREF = true, bool SPLIT = false, bool PROBE = false>
 __global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
             const unsigned n = (jt + jj * TPG) * B + q;
-            if (n < nsig) orow[n] = chirp_out<S>(xr[jj], xi[jj], ch[n]);
+            if (n < nsig) orow[n] = chirp_out<S>(xr[jj], xi[jj], PROBE ? make_double2(1.0, 0.0) : ch[n]);
         }
     }
 }
@@ -344,7 +345,8 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
         fn = sgn == 1 ? (T == 8 ? k_bmid<8, 1> : T == 4 ? k_bmid<4, 1> : T == 2 ? k_bmid<2, 1> : k_bmid<1, 1>)
                       : (T == 8 ? k_bmid<8, -1> : T == 4 ? k_bmid<4, -1> : T == 2 ? k_bmid<2, -1> : k_bmid<1, -1>);
     else if (T == 8 && !env("HSFFT_BLUE_PREF", 0)) /* c4: 20.98 vs 20.26 GS/s with the prefetch (spills) */
-        fn = sgn == 1 ? k_blast<8, 1, false> : k_blast<8, -1, false>;
+        fn = env("HSFFT_BLUE_PROBE", 0) ? (sgn == 1 ? k_blast<8, 1, false, false, true> : k_blast<8, -1, false, false, true>)
+                                        : (sgn == 1 ? k_blast<8, 1, false> : k_blast<8, -1, false>);
     else
         fn = sgn == 1 ? (T == 8 ? k_blast<8, 1> : T == 4 ? k_blast<4, 1> : T == 2 ? k_blast<2, 1> : k_blast<1, 1>)
                       : (T == 8 ? k_blast<8, -1> : T == 4 ? k_blast<4, -1> : T == 2 ? k_blast<2, -1> : k_blast<1, -1>);
@@ -362,7 +364,10 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     a.nsig = nsig;
     a.batch = batch;
     a.tiles = a.tiles_q = 512 / 8;
-    a.tile_major = env("HSFFT_BLUE_XT", 1) ? 1 : 0; /* c4 20.9 -> 21.4; tiles % 8 == 0: grid % 8 == 0 */
+    /* HSFFT_BLUE_XT bit 0 first, bit 1 middle, bit 2 last kernel: XCD-owned tiles (c4 under rocprof:
+     * mask 0 21.05, 7 21.37, 3 22.11 GS/s -- the last kernel reads in natural order; earlier 20.9 -> 21.4
+     * with all three; tiles % 8 == 0, so grid % 8 == 0) */
+    a.tile_major = (env("HSFFT_BLUE_XT", 3) >> (which == 2 ? 0 : which == 0 ? 1 : 2)) & 1;
     const long long grid = a.tiles * ((batch + T - 1) / T);
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     /* image + twiddle runs (k_bfirst: 511; k_bmid: 504 forward runs + 511 inverse entries) */

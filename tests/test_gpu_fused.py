@@ -181,7 +181,7 @@ def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
     monkeypatch.setenv("HSFFT_BLUE_PF", mask)
     monkeypatch.setenv("HSFFT_BLUE_T", t)
     monkeypatch.setenv("HSFFT_BLUE_PREF", pref)
-    monkeypatch.setenv("HSFFT_BLUE_XT", "0" if t == "2" else "1")  # both block orders
+    monkeypatch.setenv("HSFFT_BLUE_XT", "0" if t == "2" else "3")  # both block orders
     x = T.complex_input(n, 0xB1 ^ n, batch=5).reshape(5, n)
     for sgn in (1, -1):
         p = hsfft.Plan(n, sgn)
