@@ -1,0 +1,325 @@
+/*
+ * hsfft_blue_xcd.h -- Bluestein M = 2^18 = [8,8,8 | 8,8,8] (BASELINE config 4) as ONE
+ * persistent launch in which a group of 64 workgroups carries a row through all three of
+ * bpf's kernels (hsfft_blue_pf.h: chirped forward first pass, fused middle, chirp-store last
+ * pass), handing the two M-point intermediates over inside the launch.
+ *
+ * Why (measured, round 2, c4 = 99991 x 8192): the three row-looped kernels take 1.24 / 2.11 /
+ * 1.52 ms per 1024 rows with the intermediates in HBM, 0.91 / 1.29 / 1.17 ms with every row
+ * aliased to one on-die image (HSFFT_DEV_ALIAS=2, timing only) -- 21 vs 31 GSamples/s.  A
+ * group holds ONE row in flight (two 4 MiB images), so the eight groups' intermediates (64 MiB)
+ * stay in the 256 MiB Infinity Cache instead of crossing HBM twice per row.
+ *
+ * Geometry: grid = NG x 64 workgroups of 512 threads, two per CU (81.7 KiB LDS each), all
+ * co-resident (checked on the host with the occupancy API).  Workgroup w is tile w / NG of
+ * group w % NG (under round-robin dispatch group x lives on XCD x when NG == 8: speed only);
+ * group x transforms rows x, x + NG, ...  Per row:
+ *   P1  columns m0 .. m0+7 of the chirped, zero-padded input  -> image 1 rows m0 .. m0+7
+ *   --  group barrier A (all 64 tiles of image 1 written)
+ *   P2  q-columns q0 .. q0+7 of image 1: forward second pass, hk product, inverse first pass
+ *       -> image 2 rows q0 .. q0+7
+ *   --  group barrier B
+ *   P3  q-columns of image 2: inverse second pass, chirp product -> output row (n < N)
+ * P1 of the next row overwrites image 1 only after barrier B (every P2 read of it is done) and
+ * P2 of the next row overwrites image 2 only after the next barrier A (every P3 read is done).
+ *
+ * The twiddles are loaded once per launch: tw[0, 511) (P1's stages and P2's inverse first
+ * pass) and the tile's forward runs (P2; conjugated for P3) in LDS, the tile's stage-2
+ * twiddles in registers.
+ *
+ * Hand-off (MI355X_MICROARCH.md visibility table, row 1; as hsfft_fused2.h): images are
+ * written with sc1 stores, every wave waits vmcnt(0), a workgroup barrier, one lane adds 1
+ * (relaxed, agent scope) to the group's counter; waiters poll it (relaxed agent loads, bounded
+ * by a ~10 s real-time deadline that sets the sticky error word), join a barrier and read the
+ * image with sc1 loads.
+ *
+ * Arithmetic: the exact operation sequence of k_bfirst / k_bmid / k_blast (pf::stage,
+ * r8::exchange, spec, chirp_out) -- bit-identical to them and to the CPU reference
+ * (ref src/highSpeedFFT.c:1735-1907).
+ */
+#pragma once
+
+namespace bxc {
+
+constexpr unsigned NTILE = 64;  /* 8-column tiles of the 512 x 512 image = workgroups per group */
+constexpr unsigned CS = 32;     /* counter stride (128-B line per counter) */
+constexpr unsigned IMG = 512u * 512u; /* points per M-point image */
+constexpr unsigned NIMG = 4;          /* images per group: image 1 and image 2, double-buffered */
+constexpr size_t LDS_BYTES = (size_t)(512 * 8 + 511 + 504) * 16 + 16;
+
+struct XArgs {
+    const double2 *in;
+    double2 *out;
+    const double2 *tw;    /* plan twiddles of M */
+    const double2 *chirp; /* N chirp values */
+    const double2 *hk;    /* M transformed chirp values */
+    double2 *img;         /* [ng][NIMG][IMG] */
+    long long idist, odist;
+    unsigned *cnt;        /* [ng][2] counters, CS apart */
+    unsigned *err;        /* sticky error word */
+    unsigned batch, ng, nsig, sleep;
+    unsigned xmap;        /* 1: a group spans the XCDs (XCD x owns tiles [8x, 8x+8) of every group) */
+    unsigned *dbg;        /* optional per-workgroup trace (8 words): rows, P1, wait A, P2, wait B, P3 */
+};
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+template <bool SC1 = true>
+__device__ __forceinline__ void st_sc1(const __amdgpu_buffer_rsrc_t &rs, unsigned voff, unsigned soff, double x, double y)
+{
+    const double2 v = make_double2(x, y);
+    u4 u;
+    __builtin_memcpy(&u, &v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u, rs, voff, soff, SC1 ? 16 : 0);
+}
+
+template <bool SC1 = true>
+__device__ __forceinline__ double2 ld_sc1(const __amdgpu_buffer_rsrc_t &rs, unsigned voff, unsigned soff)
+{
+    const u4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, SC1 ? 16 : 0);
+    double2 d;
+    __builtin_memcpy(&d, &u, 16);
+    return d;
+}
+
+/* this workgroup's image stores are done: count it in */
+__device__ __forceinline__ void arrive(unsigned *c)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* wait until the group's counter reaches `target`; false on timeout (~10 s without progress
+ * of this one wait) / sticky error */
+__device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned target, unsigned *sflag)
+{
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); /* deadline per wait */
+        unsigned bad = 0;
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            for (unsigned k = 0; k < a.sleep; k++) __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > fz2::T_LIMIT ||
+                __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bad = 1;
+                break;
+            }
+        }
+        *sflag = bad;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keep the image loads below the poll */
+    return __builtin_amdgcn_readfirstlane(*sflag) == 0;
+}
+
+/* PLAIN (timing probe only, HSFFT_BX_PLAIN=1): image stores / loads without sc1 -- NOT a
+ * valid hand-off unless every workgroup of a group shares one L2 */
+template <int S, bool PLAIN = false>
+__global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    constexpr unsigned A = 512, B = 512;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    double2 *t0 = lds + P * G; /* tw[0, 511): stages L = 8, 64 of a first pass */
+    double2 *run = t0 + 511;   /* the tile's forward runs at L = B and 8B (bpf::runs_to_lds) */
+    unsigned *sflag = reinterpret_cast<unsigned *>(run + 504);
+    /* block -> (group, tile).  xmap 0: group = blockIdx % ng (ng == 8: one XCD per group under
+     * round-robin dispatch).  xmap 1: 64 consecutive blocks form a group and XCD x = blockIdx % 8
+     * owns tiles [8x, 8x+8) of every group, so the hk / chirp slices an XCD reads are 1/8 of
+     * them (L2-resident) while the images cross the fabric either way.  Speed only. */
+    const unsigned ng = a.ng;
+    unsigned grp, tile;
+    if (a.xmap) {
+        const unsigned x = blockIdx.x % 8, r = blockIdx.x / 8;
+        tile = x * 8 + r % 8;
+        grp = r / 8;
+    } else {
+        grp = blockIdx.x % ng;
+        tile = blockIdx.x / ng;
+    }
+    const unsigned tid = threadIdx.x, q0 = tile * G;
+    const unsigned nsig = a.nsig;
+
+    /* per-launch state: the tile's stage-2 twiddles (redistributed through the image); the
+     * chirp and hk values are re-read per row (L2 / Infinity-Cache hits; in registers they
+     * would spill) */
+    double2 w2[7];
+    {
+        r8::Args ta;
+        ta.tw = a.tw;
+        ta.B = B;
+        r8::load_tw_co<64>(w2, ta, (int)(tid / G), q0);
+    }
+    if (tid < 511) t0[tid] = a.tw[tid];
+    bpf::runs_to_lds<false>(run, a.tw, B, q0, tid);
+    r8::redistribute_tw(w2, lds);
+    __syncthreads();
+
+    double2 *imgs = a.img + (size_t)grp * NIMG * IMG; /* image 1 [2], image 2 [2] */
+    unsigned *cA = a.cnt + (size_t)grp * 2 * CS, *cB = cA + CS;
+    const unsigned R = grp < a.batch ? (a.batch - grp + ng - 1) / ng : 0; /* this group's rows */
+    unsigned tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}; /* debug: rows, P1, wait A, P2, wait B, P3, P1 / P2 store drain (10 ns) */
+
+    /* skewed pipeline: iteration k runs P3 of row k-2, P2 of row k-1, P1 of row k, so every
+     * barrier a phase waits for was signalled one phase earlier (the group has had a whole
+     * phase to arrive).  Images are double-buffered by row parity:
+     *   P1(k) overwrites image 1 [k&1], last read by P2(k-2): done once B(k-2) is complete,
+     *     which this workgroup awaited before P3(k-2) in this iteration;
+     *   P2(k-1) overwrites image 2 [(k-1)&1], last read by P3(k-3): every workgroup counts
+     *     itself into A(k-1) only after its P3(k-3), so A(k-1) -- awaited before P2(k-1) --
+     *     covers it.
+     * (Measured: the image stores take ~2.4 us per phase to drain before the arrive; deferring
+     * the arrive behind the next phase's loads did not hide it -- 24.6 vs 25.5 GSamples/s.) */
+#pragma unroll 1
+    for (unsigned k = 0; k < R + 2; k++) {
+        unsigned tk = a.dbg ? (unsigned)__builtin_amdgcn_s_memrealtime() : 0;
+#define BX_MARK(i)                                                              \
+    if (a.dbg) {                                                                \
+        const unsigned tn = (unsigned)__builtin_amdgcn_s_memrealtime();         \
+        tr[i] += tn - tk;                                                       \
+        tk = tn;                                                                \
+    }
+        double xr[8], xi[8];
+        double2 w[7];
+        if (k >= 2) { /* ---- P3 of row k-2: k_blast's body on image 2 [k&1], chirp store */
+            if (!await(a, cB, (k - 1) * NTILE, sflag)) return;
+            BX_MARK(4)
+            /* per-thread indices from an opaque copy of threadIdx in every phase, so the
+             * compiler does not hoist all three phases' addresses out of the loop (spills) */
+            unsigned tt = tid;
+            asm volatile("" : "+v"(tt));
+            const unsigned g = tt % G, jt = tt / G, q = q0 + g;
+            const unsigned col = (jt * B + q) * 16u;
+            const __amdgpu_buffer_rsrc_t r2 =
+                __builtin_amdgcn_make_buffer_rsrc(imgs + (2 + (k & 1)) * (size_t)IMG, 0, (int)(IMG * 16u), 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const double2 v = ld_sc1<!PLAIN>(r2, col, i * TPG * B * 16);
+                xr[i] = v.x;
+                xi[i] = v.y;
+            }
+#pragma unroll
+            for (int i = 0; i < 7; i++) {
+                const double2 v = run[7 * g + i];
+                w[i] = make_double2(v.x, -v.y);
+            }
+            pf::stage<8, -S>(xr, xi, w, false);
+            r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+#pragma unroll
+            for (int i = 0; i < 7; i++) {
+                const double2 v = run[56 * (1 + (jt & 7)) + 7 * g + i];
+                w[i] = make_double2(v.x, -v.y);
+            }
+            pf::stage<8, -S>(xr, xi, w, false);
+            r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+#pragma unroll
+            for (int i = 0; i < 7; i++) w[i] = make_double2(w2[i].x, -w2[i].y);
+            pf::stage<8, -S>(xr, xi, w, false);
+            double2 *orow = a.out + (long long)(grp + (k - 2) * ng) * a.odist;
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) {
+                const unsigned n = (jt + jj * TPG) * B + q;
+                if (n < nsig) orow[n] = bpf::chirp_out<S>(xr[jj], xi[jj], a.chirp[n]);
+            }
+            BX_MARK(5)
+            tr[0]++;
+        }
+        if (k >= 1 && k <= R) { /* ---- P2 of row k-1: k_bmid's body, image 1 -> image 2 [(k-1)&1] */
+            if (!await(a, cA, k * NTILE, sflag)) return;
+            BX_MARK(2)
+            unsigned tt = tid;
+            asm volatile("" : "+v"(tt));
+            const unsigned g = tt % G, jt = tt / G, q = q0 + g;
+            const unsigned col = (jt * B + q) * 16u, rowo = (q * P + jt) * 16u;
+            const unsigned par = (k - 1) & 1;
+            const __amdgpu_buffer_rsrc_t r1 =
+                __builtin_amdgcn_make_buffer_rsrc(imgs + par * (size_t)IMG, 0, (int)(IMG * 16u), 0x00020000);
+            const __amdgpu_buffer_rsrc_t r2 =
+                __builtin_amdgcn_make_buffer_rsrc(imgs + (2 + par) * (size_t)IMG, 0, (int)(IMG * 16u), 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const double2 v = ld_sc1<!PLAIN>(r1, col, i * TPG * B * 16);
+                xr[i] = v.x;
+                xi[i] = v.y;
+            }
+#pragma unroll
+            for (int i = 0; i < 7; i++) w[i] = run[7 * g + i];
+            pf::stage<8, S>(xr, xi, w, false);
+            r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+            double2 hko[8]; /* issued after the first exchange: fewer live registers */
+#pragma unroll
+            for (int i = 0; i < 8; i++) hko[i] = pf::ldg(a.hk + (size_t)i * TPG * B, col);
+#pragma unroll
+            for (int i = 0; i < 7; i++) w[i] = run[56 * (1 + (jt & 7)) + 7 * g + i];
+            pf::stage<8, S>(xr, xi, w, false);
+            r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+            pf::stage<8, S>(xr, xi, w2, false);
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) bpf::spec<S>(xr[jj], xi[jj], hko[jj]);
+            pf::stage<8, -S>(xr, xi, w, true);
+            r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+            pf::tw8_lds<true>(w, t0, 8, jt & 7);
+            pf::stage<8, -S>(xr, xi, w, false);
+            r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+            pf::tw8_lds<true>(w, t0, 64, jt & 63);
+            pf::stage<8, -S>(xr, xi, w, false);
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) st_sc1<!PLAIN>(r2, rowo, jj * TPG * 16, xr[jj], xi[jj]);
+            BX_MARK(3)
+            arrive(cB);
+            BX_MARK(7)
+        }
+        if (k < R) { /* ---- P1 of row k: k_bfirst's body (columns m = q) -> image 1 [k&1] */
+            unsigned tt = tid;
+            asm volatile("" : "+v"(tt));
+            const unsigned g = tt % G, jt = tt / G, q = q0 + g;
+            const unsigned rowo = (q * P + jt) * 16u;
+            const __amdgpu_buffer_rsrc_t r1 =
+                __builtin_amdgcn_make_buffer_rsrc(imgs + (k & 1) * (size_t)IMG, 0, (int)(IMG * 16u), 0x00020000);
+            const double2 *row = a.in + (long long)(grp + k * ng) * a.idist;
+            double2 hin[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const unsigned n = (jt + i * TPG) * A + q;
+                hin[i] = a.chirp[n < nsig ? n : 0];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const unsigned n = (jt + i * TPG) * A + q;
+                const bool inside = n < nsig;
+                const double2 x = row[inside ? n : 0];
+                double2 v = make_double2(0.0, 0.0);
+                if (inside) {
+                    if (S == 1) v = make_double2(x.x * hin[i].x + x.y * hin[i].y, -x.x * hin[i].y + x.y * hin[i].x);
+                    else v = make_double2(x.x * hin[i].x - x.y * hin[i].y, x.x * hin[i].y + x.y * hin[i].x);
+                }
+                xr[i] = v.x;
+                xi[i] = v.y;
+                xr[i + 4] = 0.0;
+                xi[i + 4] = 0.0;
+            }
+            pf::stage<8, S>(xr, xi, w, true);
+            r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+#pragma unroll
+            for (int i = 0; i < 7; i++) w[i] = t0[7 + 7 * (jt & 7) + i];
+            pf::stage<8, S>(xr, xi, w, false);
+            r8::exchange<8, 8, 8, TPG, P, G, false>(xr, xi, lds, jt, g);
+#pragma unroll
+            for (int i = 0; i < 7; i++) w[i] = t0[63 + 7 * (jt & 63) + i];
+            pf::stage<8, S>(xr, xi, w, false);
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) st_sc1<!PLAIN>(r1, rowo, jj * TPG * 16, xr[jj], xi[jj]);
+            BX_MARK(1)
+            arrive(cA);
+            BX_MARK(6)
+        }
+    }
+#undef BX_MARK
+    if (a.dbg && threadIdx.x == 0) {
+        unsigned *d = a.dbg + blockIdx.x * 8;
+        for (int i = 0; i < 8; i++) d[i] = tr[i];
+    }
+}
+
+}  // namespace bxc

@@ -552,6 +552,7 @@ int grid_for(long long n, int threads)
 #include "hsfft_fused.h"
 #include "hsfft_fused2.h"
 #include "hsfft_blue_pf.h"
+#include "hsfft_blue_xcd.h"
 
 extern "C" {
 
@@ -632,7 +633,7 @@ static int fz_check(void)
     if (*(volatile unsigned *)g_fz_err_host[dev] == 0) return 0;
     *g_fz_err_host[dev] = 0;
     HCHK(hipMemset(g_fz_ctr[dev] + fz::NQ, 0, sizeof(unsigned)));
-    snprintf(g_err, sizeof g_err, "fused 2^20 launch: a pass-B dependency wait timed out (results invalid)");
+    snprintf(g_err, sizeof g_err, "fused launch: an in-launch dependency wait timed out (results invalid)");
     return -2;
 }
 
@@ -857,6 +858,96 @@ int hsd_fused20b(const void *in, long long idist, void *out, long long odist, co
                     role ? "B" : "A", b1 - b0, it, mn, mx, it ? wt / it / 100.0 : 0.0, it ? wk / it / 100.0 : 0.0,
                     (last - first) / 1e5);
         }
+    }
+    return 0;
+}
+
+/* Bluestein M = 2^18 as one persistent launch (hsfft_blue_xcd.h).  img: ng x 4 x M points of
+ * scratch.  Returns 1 if not applicable (geometry, or the grid would not be co-resident). */
+int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng)
+{
+    int dev = 0;
+    HCHK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= HS_MAX_DEV) return -1;
+    if (batch < 1 || (sgn != 1 && sgn != -1) || ng < 1 || ng > 64 || nsig < 1 || nsig > (long long)bxc::IMG ||
+        img_bytes < (size_t)ng * bxc::NIMG * bxc::IMG * sizeof(double2))
+        return 1;
+    const char *pe = getenv("HSFFT_BX_PLAIN");
+    void (*fn)(bxc::XArgs) = (pe && atoi(pe)) ? (sgn == 1 ? bxc::k_bxcd<1, true> : bxc::k_bxcd<-1, true>)
+                                              : (sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>);
+    HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bxc::LDS_BYTES));
+    const int grid = ng * (int)bxc::NTILE;
+    {
+        /* every workgroup of a group must be resident at once (they wait on each other) */
+        int per_cu = 0, cus = 0;
+        HCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, 512, bxc::LDS_BYTES));
+        HCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if ((long long)per_cu * cus < grid) return 1;
+    }
+    const size_t CS = bxc::CS;
+    const size_t need = (CS + 2 * CS * (size_t)ng) * sizeof(unsigned);
+    if (g_fz_bytes[dev] < need) {
+        if (g_fz_ctr[dev]) {
+            HCHK(hipStreamSynchronize(stream()));
+            HCHK(hipFree(g_fz_ctr[dev]));
+        }
+        const size_t alloc = (need + 4095) & ~(size_t)4095;
+        HCHK(hipMalloc((void **)&g_fz_ctr[dev], alloc));
+        HCHK(hipMemset(g_fz_ctr[dev], 0, alloc));
+        g_fz_bytes[dev] = alloc;
+        if (!g_fz_err_host[dev]) {
+            HCHK(hipHostMalloc((void **)&g_fz_err_host[dev], 64, hipHostMallocDefault));
+            *g_fz_err_host[dev] = 0;
+        }
+    }
+    unsigned *ctr = g_fz_ctr[dev];
+    HCHK(hipMemsetAsync(ctr + CS, 0, 2 * CS * (size_t)ng * sizeof(unsigned), stream()));
+    bxc::XArgs a;
+    memset(&a, 0, sizeof a);
+    a.in = (const double2 *)in;
+    a.out = (double2 *)out;
+    a.tw = (const double2 *)tw;
+    a.chirp = (const double2 *)chirp;
+    a.hk = (const double2 *)hk;
+    a.img = (double2 *)img;
+    a.idist = idist;
+    a.odist = odist;
+    a.cnt = ctr + CS;
+    a.err = ctr + 8;
+    a.batch = (unsigned)batch;
+    a.ng = (unsigned)ng;
+    a.nsig = (unsigned)nsig;
+    {
+        const char *e = getenv("HSFFT_BX_SLEEP");
+        a.sleep = e ? (unsigned)atoi(e) : 1u;
+        e = getenv("HSFFT_BX_MAP");
+        a.xmap = e ? (unsigned)atoi(e) & 1u : 1u;
+    }
+    static unsigned *s_dbg = nullptr;
+    const char *dbgenv = getenv("HSFFT_BX_DEBUG");
+    const bool dbg = dbgenv && atoi(dbgenv) && grid <= 4096;
+    if (dbg) {
+        if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, 4096 * 8 * sizeof(unsigned)));
+        HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 8 * sizeof(unsigned), stream()));
+        a.dbg = s_dbg;
+    }
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
+    HCHK(hipGetLastError());
+    HCHK(hipMemcpyAsync(g_fz_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
+    if (dbg) { /* mean us per row: P1, wait A, P2, wait B, P3 */
+        static unsigned h[4096 * 8];
+        HCHK(hipStreamSynchronize(stream()));
+        HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
+        double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int w = 0; w < grid; w++)
+            for (int i = 0; i < 8; i++) t[i] += h[w * 8 + i];
+        const double rows = t[0] > 0 ? t[0] : 1;
+        fprintf(stderr,
+                "bxcd: wgs %d rows/wg %.1f  us per row: P1 %.2f (+drain %.2f) waitA %.2f P2 %.2f (+drain %.2f) waitB %.2f "
+                "P3 %.2f\n",
+                grid, t[0] / grid, t[1] / rows / 100.0, t[6] / rows / 100.0, t[2] / rows / 100.0, t[3] / rows / 100.0,
+                t[7] / rows / 100.0, t[4] / rows / 100.0, t[5] / rows / 100.0);
     }
     return 0;
 }

@@ -609,7 +609,7 @@ static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long
         l.nt_load |= (nt >> 2) & 1;
         l.nt_store |= (nt >> 3) & 1;
     }
-    if (env_int("HSFFT_DEV_ALIAS", 0)) l.idist = l.odist = 0; /* dev probe: MALL-resident timing only */
+    if (env_int("HSFFT_DEV_ALIAS", 0) & 1) l.idist = l.odist = 0; /* dev probe: MALL-resident timing only */
     int rc = hsd_run_pass(&e->pass[i], &l);
     if (rc) hs_seterr("pass %d: %s", i, hsd_errstr());
     return rc;
@@ -770,6 +770,27 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
     const int fuse = e->npass == 2 && M == 512 * 512 && p0->P == 512 && p1->P == 512 && p0->nst == 3 &&
                      p1->nst == 3 && p0->variant == HS_KV_R8X3 && p1->variant == HS_KV_R8X3 &&
                      p0->radix[0] == 8 && !env_int("HSFFT_BLUE_NOFUSE", 0);
+    /* one persistent launch per call (hsfft_blue_xcd.h): groups of 64 workgroups carry one row
+     * at a time through all three kernels, the intermediates stay on die (HSFFT_BLUE_XCD=0:
+     * three launches per chunk) */
+    const int ng = env_int("HSFFT_BLUE_XCD", 8);
+    if (fuse && ng > 0) {
+        const size_t ib = (size_t)ng * 4 * sizeof(fft_data) * (size_t)M; /* 4 images per group */
+        void *img = hs_scratch(3, ib);
+        /* launches of at most 65536 rows (the in-launch counters stay far from wrapping) */
+        int rc = img ? 0 : 1;
+        for (long long c0 = 0; c0 < batch && rc == 0; c0 += 65536) {
+            const int cb = (int)(batch - c0 < 65536 ? batch - c0 : 65536);
+            rc = hsd_blue_xcd((const fft_data *)in + c0 * idist, idist, (fft_data *)out + c0 * odist, odist, ds->d_tw,
+                              ds->d_chirp, ds->d_hk, img, ib, N, cb, e->sgn, ng);
+            if (rc == 1 && c0 > 0) rc = -1; /* applicability cannot change between chunks */
+        }
+        if (rc < 0) {
+            hs_seterr("bluestein persistent launch: %s", hsd_errstr());
+            return HSFFT_ERR_DEVICE;
+        }
+        if (rc == 0) return 0;
+    }
     /* the two M-point intermediates; halved while the allocation fails (a fuller device runs
      * in smaller chunks) */
     void *mid = NULL, *mid2 = NULL;
@@ -783,19 +804,22 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
         hs_seterr("bluestein scratch allocation of %lld bytes failed", (long long)(chunk * M * 16));
         return HSFFT_ERR_NOMEM;
     }
+    /* HSFFT_DEV_ALIAS bit 1 (timing probe only, results WRONG): every row of a chunk uses the
+     * same M-point intermediate, so the hand-offs between the three kernels stay on die */
+    const long long md = (env_int("HSFFT_DEV_ALIAS", 0) & 2) ? 0 : M;
     for (long long c0 = 0; c0 < batch && fuse; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
-        int rc = hsd_blue_first((const fft_data *)in + c0 * idist, idist, mid, M, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
+        int rc = hsd_blue_first((const fft_data *)in + c0 * idist, idist, mid, md, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
         if (rc < 0) hs_seterr("bluestein first pass: %s", hsd_errstr());
         if (rc == 1)
             rc = launch_pass(e, ds, 0, (const fft_data *)in + c0 * idist, idist, mid, M, cb, e->sgn, 0, e->sgn,
                              HS_LOAD_CHIRP, ds->d_chirp, HS_STORE_PLAIN, NULL, N);
-        if (!rc && hsd_blue_mid(mid, mid2, M, ds->d_tw, ds->d_hk, cb, e->sgn, 0, e->sgn, -1 * e->sgn, 1)) {
+        if (!rc && hsd_blue_mid(mid, mid2, md, ds->d_tw, ds->d_hk, cb, e->sgn, 0, e->sgn, -1 * e->sgn, 1)) {
             hs_seterr("bluestein middle: %s", hsd_errstr());
             rc = HSFFT_ERR_DEVICE;
         }
         if (!rc) {
-            rc = hsd_blue_last(mid2, M, (fft_data *)out + c0 * odist, odist, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
+            rc = hsd_blue_last(mid2, md, (fft_data *)out + c0 * odist, odist, ds->d_tw, ds->d_chirp, N, cb, e->sgn);
             if (rc < 0) hs_seterr("bluestein last pass: %s", hsd_errstr());
             if (rc == 1)
                 rc = launch_pass(e, ds, 1, mid2, M, (fft_data *)out + c0 * odist, odist, cb, -1 * e->sgn, 1, e->sgn,

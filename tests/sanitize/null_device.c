@@ -149,6 +149,16 @@ int hsd_blue_first(const void *in, long long idist, void *out, long long odist, 
     touch_rows_w(out, odist, odist, batch, 16);
     return 0;
 }
+int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng)
+{
+    touch_rows_r(in, idist, nsig, batch, 16);
+    touch_rows_r(chirp, 0, nsig, 1, 16);
+    touch_rows_r(hk, 0, 512 * 512, 1, 16);
+    touch_rows_w(img, 0, (long long)(img_bytes / 16), 1, 16);
+    touch_rows_w(out, odist, nsig, batch, 16);
+    return 0;
+}
 int hsd_fill_complex(void *d, int64_t count, uint64_t seed, uint64_t offset)
 {
     memset(d, 0, (size_t)count * 16);

@@ -178,6 +178,7 @@ def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
     """Bluestein with M = 2^18 (config 4's size; 65537 = 2^16+1 is the plan/exec M mismatch
     case D5, computed with its own exec-length table): the row-looped middle / last kernels
     (csrc/hsfft_blue_pf.h) for every tile-row count, odd batch, both signs, bit-exact."""
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "0")  # the three-launch path
     monkeypatch.setenv("HSFFT_BLUE_PF", mask)
     monkeypatch.setenv("HSFFT_BLUE_T", t)
     monkeypatch.setenv("HSFFT_BLUE_PREF", pref)
@@ -191,6 +192,34 @@ def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
         hsfft.synchronize()
         y = dout.to_array(np.complex128).reshape(5, n)
         assert T.bits_equal(y, _oracle(x, sgn, ("blue", n))), (n, sgn, mask, t)
+        din.free()
+        dout.free()
+        p.close()
+
+
+@pytest.mark.parametrize("ng,batch", [("8", 1), ("8", 5), ("8", 19), ("3", 7), ("1", 2)])
+@pytest.mark.parametrize("n", [99991, 65537, 131071])
+def test_bluestein_persistent_launch(n, ng, batch, monkeypatch):
+    """Bluestein M = 2^18 as one persistent launch (csrc/hsfft_blue_xcd.h: groups of 64
+    workgroups carry a row through the three passes, intermediates handed over in-launch):
+    fewer rows than groups, ragged last round, both signs -- bit-exact vs the oracle and vs
+    the three-launch path."""
+    monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
+    x = T.complex_input(n, 0xB7 ^ n ^ batch, batch=batch).reshape(batch, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, batch)
+        hsfft.synchronize()
+        y = dout.to_array(np.complex128).reshape(batch, n)
+        assert T.bits_equal(y, _oracle(x, sgn, ("bxcd", n, batch))), (n, sgn, ng, batch)
+        monkeypatch.setenv("HSFFT_BLUE_XCD", "0")
+        dout.fill_zero()
+        hsfft.exec_batched(p, din, dout, batch)
+        hsfft.synchronize()
+        assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), y)
+        monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
         din.free()
         dout.free()
         p.close()
