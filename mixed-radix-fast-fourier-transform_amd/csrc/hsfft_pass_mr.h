@@ -415,7 +415,88 @@ __device__ __forceinline__ void xchg1_f01(double *x, double *ld, int jt)
     }
 }
 
-template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01>
+/* fused01 for a row whose points [0, 2*P/R0) were prefetched into `pre` by LDS-DMA (k_row2
+ * PRE): the remaining leaf inputs (i = R0-1) are loaded from global first, then one barrier
+ * behind every wave's vmcnt(0) (all LDS-DMA has landed), then the prefetched inputs are read
+ * from LDS.  Same values, same butterflies as fused01. */
+template <int R0, int R1, int P, int TPG, bool CONJ>
+__device__ __forceinline__ void fused01p(double *xr, double *xi, const double2 *in, const double2 *ltw,
+                                         const double2 *pre, int jt, int sgn)
+{
+    constexpr int S = P / (R0 * R1), NG = cdiv(S, TPG), NBF0 = P / R0, Q = R0 * R1;
+    static_assert(R0 == 3, "prefetch layout assumes a radix-3 leaf");
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        int ml = g * TPG + jt;
+        if (NG * TPG != S && ml >= S) ml = S - 1;
+        double *yr = xr + g * Q, *yi = xi + g * Q;
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++) {
+            const double2 v = pf::ldg(in, (unsigned)(ml + S * j1 + (R0 - 1) * NBF0) * 16u);
+            yr[j1 * R0 + R0 - 1] = v.x;
+            yi[j1 * R0 + R0 - 1] = v.y;
+        }
+    }
+    /* every wave's LDS-DMA has landed: an explicit vmcnt(0) per wave, then the barrier
+     * (__syncthreads alone does not order the DMA: hipcc puts its vmcnt(0) after s_barrier) */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        int ml = g * TPG + jt;
+        if (NG * TPG != S && ml >= S) ml = S - 1;
+        double *yr = xr + g * Q, *yi = xi + g * Q;
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++)
+#pragma unroll
+            for (int i = 0; i < R0 - 1; i++) {
+                const double2 v = pre[ml + S * j1 + i * NBF0];
+                yr[j1 * R0 + i] = v.x;
+                yi[j1 * R0 + i] = v.y;
+            }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        double *yr = xr + g * Q, *yi = xi + g * Q;
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++) hsb::bfly<R0>(&yr[j1 * R0], &yi[j1 * R0], sgn, true);
+        double zr[Q], zi[Q];
+#pragma unroll
+        for (int kloc = 0; kloc < R0; kloc++) {
+#pragma unroll
+            for (int i = 0; i < R1; i++) {
+                zr[kloc * R1 + i] = yr[i * R0 + kloc];
+                zi[kloc * R1 + i] = yi[i * R0 + kloc];
+            }
+            const bool skip = (R1 == 4 || R1 == 5 || R1 == 7) && kloc == 0;
+            if (!skip) {
+#pragma unroll
+                for (int i = 1; i < R1; i++) {
+                    const double2 t = ltw[(R0 - 1) + (i - 1) * R0 + kloc];
+                    hsb::twmul(zr[kloc * R1 + i], zi[kloc * R1 + i], t.x, CONJ ? -t.y : t.y);
+                }
+            }
+            hsb::bfly<R1>(&zr[kloc * R1], &zi[kloc * R1], sgn, false);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            yr[q] = zr[q];
+            yi[q] = zi[q];
+        }
+    }
+}
+
+/* one 16-B-per-lane LDS-DMA: lane l copies g[l] to lds_base + 16 l (lds_base wave-uniform) */
+__device__ __forceinline__ void glds16(const double2 *g, double2 *lds_base)
+{
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                     (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
+}
+
+/* points of the next row prefetched by k_row2<..., PRE>: 132 wave-instructions of 64 */
+constexpr int ROW_PRE_PTS = 8448;
+
+template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     using LS = List6<R0, R1, R2, R3, R4, R5>;
@@ -423,7 +504,12 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     constexpr int NM0 = LS::template nmax<TPG>(), NMF = cdiv(P / (R0 * R1), TPG) * R0 * R1;
     constexpr int NM = F01 && NMF > NM0 ? NMF : NM0;
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
-    double2 *ltw = reinterpret_cast<double2 *>(ldsd + P + (P & 1));
+    /* PRE: [ltw | exchange image + prefetch area]; else [exchange image | ltw] */
+    static_assert(!PRE || (F01 && NT % 2 == 0 && 2 * NT * 8 + ROW_PRE_PTS * 16 <= 160 * 1024 &&
+                           ROW_PRE_PTS >= 2 * (P / R0) && P * 8 <= ROW_PRE_PTS * 16),
+                  "row prefetch layout");
+    double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + P + (P & 1));
+    double *img = PRE ? ldsd + 2 * NT : ldsd;
     const int jt0 = threadIdx.x, sgn = a.sgn;
     /* LDS copy of the stage-1..4 twiddles, transposed within each stage's block [L-1, RL-1):
      * entry (k, i) at L-1 + (i-1)*L + k, so the lanes of a wave (consecutive k) read
@@ -447,6 +533,7 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
      * needs a barrier of its own (once per workgroup) */
     __syncthreads();
     unsigned tp = (unsigned)__builtin_amdgcn_s_memrealtime();
+    bool pre = false; /* PRE: this row's points [0, ROW_PRE_PTS) are in the image area */
 #pragma unroll 1
     for (unsigned b = blockIdx.x; b < (unsigned)a.batch; b += gridDim.x) {
         int jt = jt0;
@@ -455,13 +542,16 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         double2 *out = a.out + (long long)b * a.odist;
         double xr[NM], xi[NM];
         if constexpr (F01) {
-            fused01<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, ldsd, jt, sgn);
+            if (PRE && pre)
+                fused01p<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, reinterpret_cast<const double2 *>(img), jt, sgn);
+            else
+                fused01<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, img, jt, sgn);
             if (a.dbg) {
                 r8::pin(*reinterpret_cast<double(*)[8]>(xr));
                 mark(a, tp, 0); /* loads + stages 0-1 */
             }
-            xchg1_f01<R0, R1, R2, P, TPG>(xr, ldsd, jt);
-            xchg1_f01<R0, R1, R2, P, TPG>(xi, ldsd, jt);
+            xchg1_f01<R0, R1, R2, P, TPG>(xr, img, jt);
+            xchg1_f01<R0, R1, R2, P, TPG>(xi, img, jt);
             mark(a, tp, 1);
         } else {
             {
@@ -479,23 +569,38 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
                 }
             }
             rstage<R0, 1, P, TPG, true, CONJ>(xr, xi, ltw, jt, sgn);
-            xchg_split<R0, 1, R1, P, TPG>(xr, xi, ldsd, jt);
+            xchg_split<R0, 1, R1, P, TPG>(xr, xi, img, jt);
             rstage<R1, LS::Lloc(1), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
-            xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, ldsd, jt);
+            xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, img, jt);
         }
         rstage<R2, LS::Lloc(2), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
-        xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, ldsd, jt);
+        xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, img, jt);
         mark(a, tp, 2);
         rstage<R3, LS::Lloc(3), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
-        xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, ldsd, jt);
+        xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, img, jt);
         mark(a, tp, 3);
         rstage<R4, LS::Lloc(4), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(4) - 1), jt, sgn);
-        xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, ldsd, jt);
+        xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, img, jt);
         mark(a, tp, 4);
         rstage<R5, LS::Lloc(5), P, TPG, false, CONJ>(xr, xi, a.tw + (LS::Lloc(5) - 1), jt, sgn);
         if (a.dbg) {
             r8::pin(*reinterpret_cast<double(*)[8]>(xr));
             mark(a, tp, 5); /* last stage (global twiddles) */
+        }
+        if constexpr (PRE) {
+            /* the image is free once every wave has read its last exchange: prefetch the next
+             * row's first ROW_PRE_PTS points into it by LDS-DMA while this row is stored */
+            const unsigned bn = b + gridDim.x;
+            pre = bn < (unsigned)a.batch;
+            if (pre) {
+                __syncthreads();
+                const double2 *inn = a.in + (long long)bn * a.idist;
+                const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+                double2 *dst = reinterpret_cast<double2 *>(img);
+#pragma unroll 1
+                for (unsigned j = wave; j < (unsigned)ROW_PRE_PTS / 64; j += TPG / 64)
+                    glds16(inn + j * 64 + lane, dst + j * 64);
+            }
         }
         constexpr int LL = LS::Lloc(5), NBFL = P / R5, NBL = cdiv(NBFL, TPG);
 #pragma unroll
@@ -604,7 +709,13 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     if (v->row && env_row_v() == 2 && v->r[0] == 3 && v->r[1] == 3 && v->r[2] == 5 && v->r[3] == 5 && v->r[4] == 7 &&
         v->r[5] == 8) {
         constexpr int P = 12600, NT = 1574;
-        const size_t lds = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
+        /* HSFFT_ROW_PRE=1: LDS-DMA prefetch of the next row's first 8448 points into the image
+         * while this row is stored -- bit-exact, measured slower (109 vs 113.6 GSamples/s: the
+         * DMA queues behind the row's stores on the CU's memory path; load phase unchanged) */
+        const char *ep = getenv("HSFFT_ROW_PRE");
+        const bool rpre = ep ? atoi(ep) != 0 : false;
+        const size_t lds = rpre ? (size_t)NT * sizeof(double2) + (size_t)ROW_PRE_PTS * sizeof(double2)
+                                : (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
         if (l->batch <= 0) {
             snprintf(g_err, sizeof g_err, "mr: bad row batch=%d", l->batch);
             return -1;
@@ -613,6 +724,8 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         const bool f01 = ef ? atoi(ef) != 0 : true;
         kfn fn = f01 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true>)
                      : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, false> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, false>);
+        if (rpre)
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true, true>;
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));
         HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));

@@ -418,7 +418,8 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"}])
+@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"},
+                                 {"HSFFT_ROW_PRE": "1"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -427,7 +428,7 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     exactly ONE row, so no row can lean on an earlier row's barriers (the stage-1 twiddles of
     the fused first stages are read right after the per-workgroup LDS copy).  Variants:
     mr::k_row2 with stages 0-1 fused (default) and unfused, mr::k_row (one workgroup per row),
-    the two mixed-radix passes."""
+    the two mixed-radix passes, k_row2 with the next row's LDS-DMA prefetch."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600
