@@ -539,12 +539,16 @@ def main():
     ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
     ent = traffic_entry(args.config)
     kern = ent.get("kernel", "").replace("void ", "") if ent.get("batch") == batch else ""
+    launches = f"{max(npass, 1)} launch(es)"
+    if kind == "c2c" and plan.header()["lt"] != 0 or args.config == "c4":  # Bluestein
+        launches = ("one persistent launch (bxc::k_bxcd) per 65536 rows"
+                    if os.environ.get("HSFFT_BLUE_XCD", "8") != "0" else "3 launches per 1024-row chunk")
     out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(args.config, batch),
                        "algorithmic_bytes": samples * bytes_per_sample,
-                       "basis": f"whole step: {bytes_per_sample} B x N x batch / event-timed step time, all "
-                                f"{max(npass, 1)} launch(es) of the step",
-                       "kernel": kern or f"{max(npass, 1)} launch(es) per step"}
+                       "basis": f"whole step: {bytes_per_sample} B x N x batch / event-timed step time, "
+                                f"{launches} of the step",
+                       "kernel": kern or f"{launches} per step"}
     if pass_ms:
         out["roofline"]["pass_ms"] = [round(p, 4) for p in pass_ms]
         out["roofline"]["pass_frac"] = [round(samples * bytes_per_sample / (p / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
