@@ -426,9 +426,14 @@ __device__ __forceinline__ void r2c_load(double (&xr)[8], double (&xi)[8], doubl
     const unsigned lane0 = ((tid0 >> 3) * B + q0 + (tid0 & 7)) * 16u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
-        xr[i] = v.x;
-        xi[i] = v.y;
+        if constexpr (PROBE & 8) { /* timing probe: no data loads */
+            xr[i] = (double)(lane0 + i);
+            xi[i] = (double)(q0 - i);
+        } else {
+            const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
+            xr[i] = v.x;
+            xi[i] = v.y;
+        }
     }
     r8::Args ta;
     ta.tw = tw;
@@ -471,7 +476,8 @@ __device__ __forceinline__ void r2c_stages(double (&xr)[8], double (&xi)[8], con
 }
 
 /* PROBE (timing only, HSFFT_R2C_PROBE; results WRONG): bit 0 twiddle2 not loaded, bit 1
- * stage-2 twiddles not loaded -- what the twiddle traffic costs */
+ * stage-2 twiddles not loaded, bit 2 no output stores, bit 3 no data loads -- what each
+ * stream costs */
 template <int SGN, bool COMPACT, int PROBE = 0>
 __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
 {
@@ -511,11 +517,22 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
             const double2 zk = make_double2(xr[jj], xi[jj]), zh = make_double2(ld[4096 + s], ld[s]);
             double re, im;
             r8::r2c_pair(zk, zh, (PROBE & 1) ? make_double2(1.0, 0.0) : w2t[k], re, im);
-            X[k] = make_double2(re, im);
-            if (!COMPACT) X[N - k] = make_double2(re, -im);
+            const bool st = !(PROBE & 4) || re == -7.25e300; /* PROBE bit 2: no stores */
+            /* bit 4: no stores to the line-straddling streams X[k], X[h+k]; bit 5: none to the
+             * aligned X[N-k], X[h-k] */
+            const bool sm = st && (!(PROBE & 16) || re == -7.25e300), sa = st && (!(PROBE & 32) || re == -7.25e300);
+            /* bit 6: non-temporal output stores */
+#define R2C_ST(idx, v)                                  \
+    do {                                                \
+        if (PROBE & 64) stg_nt(X, (idx) * 16u, (v));    \
+        else X[idx] = (v);                              \
+    } while (0)
+            if (sm) R2C_ST(k, make_double2(re, im));
+            if (!COMPACT && sa) R2C_ST(N - k, make_double2(re, -im));
             r8::r2c_pair(zh, zk, (PROBE & 1) ? make_double2(1.0, 0.0) : w2t[hk], re, im);
-            X[hk] = make_double2(re, im);
-            if (!COMPACT) X[N - hk] = make_double2(re, -im);
+            if (sa || re == -7.25e300) R2C_ST(hk, make_double2(re, im));
+            if (!COMPACT && (sm || re == -7.25e300)) R2C_ST(N - hk, make_double2(re, -im));
+#undef R2C_ST
         }
     } else { /* column 0: k = u*B pairs with (P-u)*B */
         r2c_load<PROBE>(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
@@ -567,10 +584,21 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
                                          : (sgn == 1 ? k_r2c_fused<1, false> : k_r2c_fused<-1, false>);
     {
         const char *pe = getenv("HSFFT_R2C_PROBE");
-        const int pr = pe ? atoi(pe) & 3 : 0;
-        if (pr == 1 && sgn == 1 && !compact) fn = k_r2c_fused<1, false, 1>;
-        if (pr == 2 && sgn == 1 && !compact) fn = k_r2c_fused<1, false, 2>;
-        if (pr == 3 && sgn == 1 && !compact) fn = k_r2c_fused<1, false, 3>;
+        const int pr = pe ? atoi(pe) & 127 : 0;
+        if (sgn == 1 && !compact) switch (pr) {
+            case 1: fn = k_r2c_fused<1, false, 1>; break;
+            case 2: fn = k_r2c_fused<1, false, 2>; break;
+            case 3: fn = k_r2c_fused<1, false, 3>; break;
+            case 4: fn = k_r2c_fused<1, false, 4>; break;
+            case 7: fn = k_r2c_fused<1, false, 7>; break;
+            case 8: fn = k_r2c_fused<1, false, 8>; break;
+            case 12: fn = k_r2c_fused<1, false, 12>; break;
+            case 15: fn = k_r2c_fused<1, false, 15>; break;
+            case 16: fn = k_r2c_fused<1, false, 16>; break;
+            case 32: fn = k_r2c_fused<1, false, 32>; break;
+            case 64: fn = k_r2c_fused<1, false, 64>; break;
+            default: break;
+            }
     }
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a, (unsigned)h);
