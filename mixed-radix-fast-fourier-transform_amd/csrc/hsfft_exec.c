@@ -126,7 +126,15 @@ static int build_passes_pow2(hs_entry *e)
     int n8 = e->nst - 1;            /* radix-8 stages after stage 0 */
     /* at most 4 stages per pass; P <= 2048 unless r0 == 8 and a 4096-point first pass
      * saves a whole pass (2^21 = [8,8,8,8] + [8,8,8]) */
-    const int k1max = r0 == 8 ? (n8 == 6 ? 3 : 2) : 3;
+    int k1max = r0 == 8 ? (n8 == 6 ? 3 : 2) : 3;
+    /* the whole transform as ONE pass when it fits one workgroup (P <= 8192 points, <= 1024
+     * threads of 8 points): one HBM round trip instead of two -- 4096 = [8,8,8,8] and
+     * 8192 = [2,8,8,8,8] (HSFFT_WHOLE=0: the two-pass schedule) */
+    {
+        long long pall = r0;
+        for (int i = 0; i < n8; i++) pall *= 8;
+        if (n8 <= 4 && pall <= 8192 && env_int("HSFFT_WHOLE", 1) && r8_has_variant(r0, n8, 1, 1, 1)) k1max = n8;
+    }
     /* number of later passes needed if the first takes k1 eights: ceil((n8-k1)/3) */
     int best_k1 = -1, best_np = 1 << 30, best_bal = 1 << 30;
     for (int k1 = r0 == 8 ? 0 : 1; k1 <= k1max && k1 <= n8; k1++) { /* every pass needs P >= 8 */

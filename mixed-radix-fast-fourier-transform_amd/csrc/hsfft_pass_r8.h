@@ -242,6 +242,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (occ_hint<R0, N8, G, FIRS
 {
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG, WM = G / WQ;
+    static_assert(N8 <= 4 && TPG * G <= 1024, "pass shape");
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
 
     /* block -> (row b, tile): 32-bit arithmetic (64-bit division expands to long loops) */
@@ -304,7 +305,13 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (occ_hint<R0, N8, G, FIRS
             load_tw<8, S::Lloc(3), TPG>(wa, a, jt, q, valid);
             do_stage<8, S::Lloc(3), TPG>(xr, xi, wa, a, jt, q, false);
         }
+        if constexpr (N8 >= 4) { /* whole-row 8192 = [2,8,8,8,8] */
+            exchange<8, S::Lloc(3), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            load_tw<8, S::Lloc(4), TPG>(wa, a, jt, q, valid);
+            do_stage<8, S::Lloc(4), TPG>(xr, xi, wa, a, jt, q, false);
+        }
     } else {
+    static_assert(N8 <= 3, "later passes have at most three radix-8 stages");
     if constexpr (!FIRST) load_tw<R0, 1, TPG>(wa, a, jt, q, valid);
     if constexpr (N8 >= 1) {
         if constexpr (CTW) load_tw_co<S::Lloc(1)>(wb, a, jt, q0);
@@ -634,7 +641,7 @@ static const Variant k_variants[] = {
     /* first passes (B == 1): WQ = 1, G = WM */
     R8V(4, 3, 1, 1, true), R8V(4, 3, 2, 1, true), R8V(4, 3, 4, 1, true),
     R8V(2, 3, 1, 1, true), R8V(2, 3, 2, 1, true), R8V(2, 3, 4, 1, true),
-    R8V(8, 3, 1, 1, true), R8V(8, 3, 2, 1, true),
+    R8V(8, 3, 1, 1, true), R8V(8, 3, 2, 1, true), R8V(2, 4, 1, 1, true), /* 8192 = [2,8,8,8,8] whole row */
     R8V(8, 2, 1, 1, true), R8V(8, 2, 2, 1, true), R8V(8, 2, 4, 1, true), R8V(8, 2, 8, 1, true),
     R8V(4, 2, 1, 1, true), R8V(4, 2, 4, 1, true), R8V(4, 2, 8, 1, true),
     R8V(2, 2, 1, 1, true), R8V(2, 2, 4, 1, true), R8V(2, 2, 8, 1, true),

@@ -59,6 +59,29 @@ C2C_SIZES = [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 19, 20, 22, 25, 27,
              97, 100, 121, 125, 128, 243, 256, 343, 512, 1021, 1024, 4096, 5003, 12600, 65536]
 
 
+@pytest.mark.parametrize("whole", ["1", "0"])
+@pytest.mark.parametrize("n", [2048, 4096, 8192, 16384])
+def test_pow2_whole_row_single_pass(n, whole, monkeypatch):
+    """powers of two that fit one workgroup (4096 = [8,8,8,8], 8192 = [2,8,8,8,8]) run as ONE
+    pass (one HBM round trip); HSFFT_WHOLE=0 keeps the two-pass schedule.  Bit-exact both ways,
+    both signs, ragged batch."""
+    monkeypatch.setenv("HSFFT_WHOLE", whole)
+    rows = 5
+    x = T.complex_input(n, 0x5150 ^ n, batch=rows).reshape(rows, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        single = n <= 2048 or (whole == "1" and n <= 8192)
+        assert p.num_passes() == (1 if single else 2), (n, whole)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, rows)
+        y = dout.to_array(np.complex128).reshape(rows, n)
+        assert T.bits_equal(y, oracle_rows(x, sgn)), (n, sgn, whole)
+        din.free()
+        dout.free()
+        p.close()
+
+
 @pytest.mark.parametrize("n", C2C_SIZES)
 def test_c2c_dropin_host_pointers_bit_exact(n):
     """fft_exec with host buffers (the reference's own calling convention)."""
