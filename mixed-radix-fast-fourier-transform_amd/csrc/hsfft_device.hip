@@ -1102,7 +1102,7 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     a.tiles = tm * tq;
     long long grid = a.tiles * l->batch;
     size_t lds = 2 * (size_t)p->P * p->G * sizeof(double2);
-    if (grid <= 0 || grid > 0x7fffffffLL || lds > 65536) {
+    if (grid <= 0 || grid > 0x7fffffffLL || lds > 160 * 1024) {
         snprintf(g_err, sizeof g_err, "hsd_run_pass: bad launch geometry (grid %lld, lds %zu)", grid, lds);
         return -1;
     }
@@ -1131,6 +1131,7 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     case 53: fn = k_pass_generic<53>; break;
     default: fn = k_pass_generic<-1>; break;
     }
+    if (lds > 65536) HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(256), lds, stream(), a);
     HCHK(hipGetLastError());
     return 0;

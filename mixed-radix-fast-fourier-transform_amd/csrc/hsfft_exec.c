@@ -235,7 +235,17 @@ static int build_passes(hs_entry *e)
             return 0;
         }
     }
-    const int pmax = pass_pmax();
+    /* a whole row that fits the generic kernel's LDS ping-pong (32 B per point <= 160 KiB):
+     * one pass, one HBM round trip, instead of passes of <= Pmax points (HSFFT_WHOLE=0) */
+    int odd = 0, nodd = 0; /* distinct odd radices >= 11 (the generic kernel specialises one) */
+    for (int i = 0; i < e->nst; i++) {
+        const int r = e->stage_r[i];
+        if (r == 2 || r == 3 || r == 4 || r == 5 || r == 7 || r == 8 || r == odd) continue;
+        odd = r;
+        nodd++;
+    }
+    const int whole = env_int("HSFFT_WHOLE", 1) && e->M <= 5120 && e->nst <= HS_MAX_PASS_STAGES && nodd <= 1;
+    const int pmax = whole ? e->M : pass_pmax();
     int s = 0, np = 0;
     long long B = 1;
     while (s < e->nst) {

@@ -82,6 +82,26 @@ def test_pow2_whole_row_single_pass(n, whole, monkeypatch):
         p.close()
 
 
+@pytest.mark.parametrize("whole", ["1", "0"])
+@pytest.mark.parametrize("n", [1000, 2000, 3000, 5000, 5120, 243, 625, 1001, 2 * 3 * 5 * 7 * 8, 11 * 13 * 8, 4913])
+def test_mixed_whole_row_single_pass(n, whole, monkeypatch):
+    """mixed / odd sizes up to 5120 points: ONE generic LDS pass per row (HSFFT_WHOLE=1,
+    default) or passes of <= 512 points; bit-exact both ways, both signs."""
+    monkeypatch.setenv("HSFFT_WHOLE", whole)
+    rows = 3
+    x = T.complex_input(n, 0x3A3A ^ n, batch=rows).reshape(rows, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, rows)
+        y = dout.to_array(np.complex128).reshape(rows, n)
+        assert T.bits_equal(y, oracle_rows(x, sgn)), (n, sgn, whole, p.num_passes())
+        din.free()
+        dout.free()
+        p.close()
+
+
 @pytest.mark.parametrize("n", C2C_SIZES)
 def test_c2c_dropin_host_pointers_bit_exact(n):
     """fft_exec with host buffers (the reference's own calling convention)."""
