@@ -282,8 +282,8 @@ __device__ void stage_oddT(const KArgs &a, const double2 *src, double2 *dst, int
 
 /* OR: 0 = no odd radix in the pass, > 0 = the pass's only odd radix (compile-time stage,
  * registers sized for that radix), -1 = several odd radices (runtime stage_odd) */
-template <int OR>
-__global__ __launch_bounds__(256) void k_pass_generic(KArgs a)
+template <int OR, int NT = 256>
+__global__ __launch_bounds__(NT) void k_pass_generic(KArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const long long blk = blockIdx.x;
@@ -1131,8 +1131,26 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     case 53: fn = k_pass_generic<53>; break;
     default: fn = k_pass_generic<-1>; break;
     }
+    /* tiles of >= 1536 points (whole rows up to 5120): 1024 threads instead of 256 -- at 48-160
+     * KiB of LDS a CU holds 1-3 workgroups, so 256 threads left it with 4-12 waves
+     * (measured: 3000 33.6 -> 56.0, 5000 36.5 -> 64.4, 17^3 31.2 -> 50.7 GSamples/s; HSFFT_GNT=256) */
+    int nt = 256;
+    {
+        const char *e = getenv("HSFFT_GNT");
+        const int want = e ? atoi(e) : 1024;
+        if (want >= 1024 && (long long)p->P * p->G >= 1536) {
+            nt = 1024;
+            switch (oddr) { /* the variants whose registers fit 1024 threads (<= 128 VGPRs) */
+            case 0: fn = k_pass_generic<0, 1024>; break;
+            case 11: fn = k_pass_generic<11, 1024>; break;
+            case 13: fn = k_pass_generic<13, 1024>; break;
+            case 17: fn = k_pass_generic<17, 1024>; break;
+            default: nt = 256; break;
+            }
+        }
+    }
     if (lds > 65536) HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(256), lds, stream(), a);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(nt), lds, stream(), a);
     HCHK(hipGetLastError());
     return 0;
 }

@@ -408,6 +408,22 @@ static hs_entry *entry_build(const struct fft_set *o)
             free(e);
             return NULL;
         }
+        if (env_int("HSFFT_PLAN_DEBUG", 0)) { /* dev: the pass schedule */
+            fprintf(stderr, "hsfft plan N=%d M=%d:", e->N, e->M);
+            for (int i = 0; i < e->npass; i++) {
+                const hsd_pass *p = &e->pass[i];
+                fprintf(stderr, " [P=%d r=", p->P);
+                for (int s = 0; s < p->nst; s++) fprintf(stderr, "%s%d", s ? "," : "", p->radix[s]);
+                fprintf(stderr, " A=%lld B=%lld G=%d Wq=%d v=%d]", (long long)p->A, (long long)p->B, p->G, p->Wq, p->variant);
+            }
+            fprintf(stderr, "\n");
+        }
+        if (0) {
+            free(e->tw_private);
+            free(e->gcs);
+            free(e);
+            return NULL;
+        }
     }
     if (o->lt == 1) { /* chirp h(n) = exp(i*pi*n^2/N), ref :1674-1690 */
         const double PI = 3.1415926535897932384626433832795;
