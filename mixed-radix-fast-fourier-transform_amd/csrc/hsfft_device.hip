@@ -1131,14 +1131,16 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     case 53: fn = k_pass_generic<53>; break;
     default: fn = k_pass_generic<-1>; break;
     }
-    /* tiles of >= 1536 points (whole rows up to 5120): 1024 threads instead of 256 -- at 48-160
-     * KiB of LDS a CU holds 1-3 workgroups, so 256 threads left it with 4-12 waves
-     * (measured: 3000 33.6 -> 56.0, 5000 36.5 -> 64.4, 17^3 31.2 -> 50.7 GSamples/s; HSFFT_GNT=256) */
+    /* whole rows of >= 1536 points (up to 5120): 1024 threads instead of 256 -- at 48-160 KiB
+     * of LDS a CU holds 1-3 workgroups, so 256 threads left it with 4-12 waves (measured: 3000
+     * 33.6 -> 56.0, 5000 36.5 -> 64.4, 17^3 31.2 -> 50.7 GSamples/s; the first pass of 100000
+     * (P = 500, 4 columns) 32.6 -> 26.4, so passes of a multi-pass schedule keep 256;
+     * HSFFT_GNT=256 everywhere) */
     int nt = 256;
     {
         const char *e = getenv("HSFFT_GNT");
         const int want = e ? atoi(e) : 1024;
-        if (want >= 1024 && (long long)p->P * p->G >= 1536) {
+        if (want >= 1024 && (long long)p->P * p->G >= 1536 && p->A == 1 && p->B == 1) {
             nt = 1024;
             switch (oddr) { /* the variants whose registers fit 1024 threads (<= 128 VGPRs) */
             case 0: fn = k_pass_generic<0, 1024>; break;
