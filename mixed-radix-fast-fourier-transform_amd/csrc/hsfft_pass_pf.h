@@ -560,6 +560,184 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
     }
 }
 
+/* ------------------------------------------------------------------ r2c split, tile walk
+ * Same split and arithmetic as k_r2c_fused, rearranged so that every output line is written
+ * whole.  Why: the lo tile's columns [8j+1, 8j+9) put the X[k] and X[h+k] streams one entry
+ * off the 128-B lines (7 entries in line j, 1 in line j+1), and a line written in two parts by
+ * two workgroups costs ~3x an aligned one (tools/experiments/r2c_stores.hip: 4 streams, no
+ * arithmetic, 10.5 ms per 512 rows with two such streams, 5.3 ms with all four aligned).
+ * Here a 1024-thread workgroup walks T consecutive tile pairs j of one row: threads [0, 512)
+ * transform the lo tile and threads [512, 1024) the hi tile at the same time (one exchange
+ * image each), each half computes its own half of the pair outputs (lo: X[k], X[N-k]; hi:
+ * X[h-k], X[h+k]), and the two off-line streams are shifted by one lane within each 8-lane
+ * group before the store: the entry that falls into line j+1 is carried (LDS, same thread)
+ * to the next tile's store, so each store instruction writes eight whole 128-B lines.  Only
+ * the first line of a walk (its entry 0 belongs to the previous walk) and the carry left at
+ * the end are partial.  Reference layout only (rows of N bins); the last walk WG of a row
+ * index W handles column 0. */
+__device__ __forceinline__ void r2cw_load(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned B, unsigned q0,
+                                          unsigned t)
+{
+    constexpr int TPG = 64;
+    const unsigned lane0 = ((t >> 3) * B + q0 + (t & 7)) * 16u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
+        xr[i] = v.x;
+        xi[i] = v.y;
+    }
+}
+
+/* the tile's twiddles (stage-0/1 runs -> ltw, stage-2 coalesced + redistributed) and its
+ * three stages; the tile's points are in xr/xi (loaded earlier, possibly still in flight) */
+template <int SGN>
+__device__ __forceinline__ void r2cw_tile(double (&xr)[8], double (&xi)[8], unsigned B, unsigned q0,
+                                          const double2 *tw, double2 *img, double2 *ltw, unsigned t)
+{
+    constexpr int P = 512, G = 8;
+    double2 w2[7];
+    {
+        r8::Args ta;
+        ta.tw = tw;
+        ta.B = B;
+        r8::load_tw_co<64>(w2, ta, (int)(t >> 3), q0);
+    }
+    __syncthreads(); /* the previous tile's readers of both images and of ltw are done */
+    if (t < 504) {
+        const unsigned r = t / 56, e = t % 56;
+        const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
+        ltw[t] = tw[src];
+    }
+    { /* r8::redistribute_tw with the wave index inside this half */
+        const unsigned lane = t & 63, wave = t >> 6;
+        double2 *reg = img + wave * 448 + (lane >> 3) * 56;
+#pragma unroll
+        for (int j = 0; j < 7; j++) reg[(lane & 7) + 8 * j] = w2[j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int i = 0; i < 7; i++) w2[i] = reg[(lane & 7) * 7 + i];
+    }
+    __syncthreads(); /* ltw written; every wave has read its twiddles back from the image */
+    r2c_stages<SGN, false>(xr, xi, w2, img, ltw, t);
+    (void)P;
+    (void)G;
+}
+
+/* lane (g-1) of this 8-lane group (DIR = -1) or lane (g+1) (DIR = +1), wrapping in the group */
+template <int DIR>
+__device__ __forceinline__ double2 grp_shift(double2 v)
+{
+    const int lane = __lane_id(), src = (lane & ~7) | ((lane + DIR) & 7);
+    return make_double2(__shfl(v.x, src, 64), __shfl(v.y, src, 64));
+}
+
+constexpr int R2CW_LDS = (2 * 4096 + 2 * 504 + 1024) * 16; /* 2 images, 2 twiddle runs, 2 carry rows */
+
+template <int SGN>
+__global__ __launch_bounds__(1024, 1) void k_r2c_walk(Args a, unsigned h, unsigned T, unsigned W)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const unsigned blk = xcd_remap(blockIdx.x), b = blk / (W + 1), s = blk % (W + 1);
+    const unsigned tid = threadIdx.x, half = tid >> 9, t = tid & 511, g = t & 7, jt = t >> 3;
+    double2 *img = lds + half * 4096, *pimg = lds + (half ^ 1) * 4096;
+    double2 *ltw = lds + 8192 + half * 504, *cry = lds + 8192 + 2 * 504 + half * 512;
+    const unsigned B = (unsigned)a.B, N = 2 * h;
+    const double2 *row = a.in + (long long)b * a.idist;
+    double2 *X = a.out + (long long)b * a.odist;
+    const double2 *w2t = a.saux;
+    double xr[8], xi[8];
+    if (s == W) { /* column 0 (k = u*B pairs with (P-u)*B): both halves transform the tile, the lo half writes */
+        r2cw_load(xr, xi, row, B, 0, t);
+        r2cw_tile<SGN>(xr, xi, B, 0, a.tw, img, ltw, t);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) img[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
+        __syncthreads();
+        if (half || g != 0) return;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B;
+            const double2 zk = make_double2(xr[jj], xi[jj]);
+            if (u == 0) {
+                X[0] = make_double2(zk.x + zk.y, 0.0);
+                X[h] = make_double2(zk.x - zk.y, 0.0);
+            } else {
+                const double2 zh = img[(P - u) * G];
+                double re, im;
+                r8::r2c_pair(zk, zh, w2t[k], re, im);
+                X[k] = make_double2(re, im);
+                X[N - k] = make_double2(re, -im);
+            }
+        }
+        return;
+    }
+    const unsigned j0 = s * T, j1 = min(j0 + T, B / 16);
+    r2cw_load(xr, xi, row, B, half ? B - 8 * j0 - 8 : 8 * j0 + 1, t);
+#pragma unroll 1
+    for (unsigned j = j0; j < j1; j++) {
+        const unsigned q0 = half ? B - 8 * j - 8 : 8 * j + 1;
+        r2cw_tile<SGN>(xr, xi, B, q0, a.tw, img, ltw, t);
+        /* the last exchange ended with a barrier: both images are free */
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) img[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
+        __syncthreads();
+        /* the next tile's points load while this tile's pairs are formed and stored (the pair
+         * loop reads this tile's points back from the image) */
+        {   /* unconditional (the last tile reloads itself): a branch around the loads makes the
+             * waitcnt pass drain vmcnt at the join */
+            const unsigned jn = j + 1 < j1 ? j + 1 : j;
+            r2cw_load(xr, xi, row, B, half ? B - 8 * jn - 8 : 8 * jn + 1, t);
+        }
+        const bool first = j == j0;
+#pragma unroll 2
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B + q0 + g; /* this thread's bin */
+            const double2 z = img[(jt + jj * TPG) * G + g], zp = pimg[(P - 1 - u) * G + (7 - g)];
+            double re, im;
+            r8::r2c_pair(z, zp, w2t[k], re, im);
+            if (!half) {
+                /* X[N-k] (aligned); X[k] = bins 8j+1+g -> line [8j, 8j+8) takes lane g-1's value,
+                 * lane 0 the entry carried from the previous tile (bin 8j) */
+                X[N - k] = make_double2(re, -im);
+                const double2 v = grp_shift<-1>(make_double2(re, im)); /* lane 0: lane 7's = next carry */
+                const unsigned p = u * B + 8 * j + g;
+                if (g != 0) X[p] = v;
+                else {
+                    if (!first) X[p] = cry[u];
+                    cry[u] = v;
+                }
+            } else {
+                /* X[h-k] = this bin (aligned); X[h+k'] (k' = the lo partner, bins 8j+8-g of row
+                 * P-1-u) -> line [8j, 8j+8) written descending: lane g takes lane g+1's value,
+                 * lane 7 the carried entry (bin 8j) */
+                X[k] = make_double2(re, im);
+                const double2 v = grp_shift<1>(make_double2(re, -im)); /* lane 7: lane 0's = next carry */
+                const unsigned p = h + (P - 1 - u) * B + 8 * j + 7 - g;
+                if (g != 7) X[p] = v;
+                else {
+                    if (!first) X[p] = cry[u];
+                    cry[u] = v;
+                }
+            }
+        }
+    }
+    /* the carry of the last tile: bin 8*j1 of the off-line streams (already written by the
+     * other stream's aligned stores when j1 is the row's last tile: column B/2) */
+    if (j1 < B / 16 && j1 > j0) {
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG;
+            if (!half && g == 0) X[u * B + 8 * j1] = cry[u];
+            if (half && g == 7) X[h + (P - 1 - u) * B + 8 * j1] = cry[u];
+        }
+    }
+}
+
+inline int env(const char *name, int dflt);
+
 /* returns 1 if not applicable, 0 on launch, < 0 on error */
 inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2,
                             long long h, long long B, int batch, int sgn, hipStream_t st, bool compact = false)
@@ -577,6 +755,18 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     a.B = B;
     a.batch = batch;
     a.tiles = a.tiles_q = B / 16 + 1;
+    /* whole-line tile walk (opt-in, HSFFT_R2C_WALK=1): bit-exact, but one 1024-thread workgroup
+     * per CU loses more overlap than the aligned stores gain (c5 95.4 vs 98.2 GSamples/s) */
+    if (!compact && env("HSFFT_R2C_WALK", 0) && !getenv("HSFFT_R2C_PROBE")) {
+        const long long T = env("HSFFT_R2C_WT", 16) > 0 ? env("HSFFT_R2C_WT", 16) : 16, W = (B / 16 + T - 1) / T;
+        const long long grid = (W + 1) * (long long)batch;
+        if (grid <= 0 || grid > 0x7fffffffLL) return -1;
+        void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk<1> : k_r2c_walk<-1>;
+        HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW_LDS));
+        hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(1024), R2CW_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
+        HCHK(hipGetLastError());
+        return 0;
+    }
     const long long grid = a.tiles * (long long)batch;
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     const size_t lds = (size_t)(512 * 8 + 504) * sizeof(double2);

@@ -461,6 +461,30 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wt", ["16", "1", "5", "4096", "walk0"])
+@pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
+def test_r2c_walk(n, sgn, wt, monkeypatch):
+    """pf::k_r2c_walk (opt-in split kernel of the reference-layout r2c): walks of WT tile pairs
+    per workgroup, whole-line stores with the one-entry carry between tiles.  WT=1: every tile
+    is a walk's first (partial first line, carry written at once); 5: walks of uneven length
+    and a short last walk; 4096: one walk per row (the carry reaches column B/2); walk0: the
+    one-tile-per-workgroup k_r2c_fused.  Bit-exact vs the oracle, odd batch."""
+    if wt == "walk0":
+        monkeypatch.setenv("HSFFT_R2C_WALK", "0")
+    else:
+        monkeypatch.setenv("HSFFT_R2C_WALK", "1")
+        monkeypatch.setenv("HSFFT_R2C_WT", wt)
+    x = T.real_input(n, 29, batch=3).reshape(3, n)
+    rp = hsfft.RealPlan(n, sgn)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(3 * n * 16)
+    hsfft.fill_complex(dout, 3 * n, 1)  # stale data: every bin must be written
+    hsfft.r2c_batched(rp, din, dout, 3)
+    y = dout.to_array(np.complex128).reshape(3, n)
+    assert T.bits_equal(y, T.oracle_r2c(x, sgn))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"},
                                  {"HSFFT_ROW_PRE": "1"}])
 @pytest.mark.parametrize("sgn", [1, -1])
