@@ -339,9 +339,26 @@ __device__ __forceinline__ void rstage(double *xr, double *xi, const double2 *tw
  * of the stage-0 butterflies ml + S*i (S = P/(R0*R1), i < R1), so the R0*R1 points of group
  * ml are closed under both stages -- a thread transforms whole groups and the first exchange
  * disappears.  Same butterflies, twiddles and operand order as the unfused stages. */
-template <int R0, int R1, int P, int TPG, bool CONJ>
+/* inputs of fused01's groups 0..PFG-1 (ml = g*TPG + jt) of a row, loaded ahead (k_row2 PF) */
+template <int R0, int R1, int P, int TPG, int PFG>
+__device__ __forceinline__ void f01_load0(double2 (&p0)[PFG * R0 * R1], const double2 *in, int jt)
+{
+    constexpr int S = P / (R0 * R1), NBF0 = P / R0;
+#pragma unroll
+    for (int g = 0; g < PFG; g++) {
+        int ml = g * TPG + jt;
+        if (ml >= S) ml = S - 1;
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++)
+#pragma unroll
+            for (int i = 0; i < R0; i++)
+                p0[(g * R1 + j1) * R0 + i] = pf::ldg(in, (unsigned)(ml + S * j1 + i * NBF0) * 16u);
+    }
+}
+
+template <int R0, int R1, int P, int TPG, bool CONJ, int HAS0 = 0>
 __device__ __forceinline__ void fused01(double *xr, double *xi, const double2 *in, const double2 *ltw, double *ld,
-                                        int jt, int sgn)
+                                        int jt, int sgn, const double2 *p0 = nullptr)
 {
     constexpr int S = P / (R0 * R1), NG = cdiv(S, TPG), NBF0 = P / R0, Q = R0 * R1;
 #pragma unroll
@@ -354,7 +371,7 @@ __device__ __forceinline__ void fused01(double *xr, double *xi, const double2 *i
         for (int j1 = 0; j1 < R1; j1++)
 #pragma unroll
             for (int i = 0; i < R0; i++) {
-                const double2 v = pf::ldg(in, (unsigned)(ml + S * j1 + i * NBF0) * 16u);
+                const double2 v = g < HAS0 ? p0[(g * R1 + j1) * R0 + i] : pf::ldg(in, (unsigned)(ml + S * j1 + i * NBF0) * 16u);
                 yr[j1 * R0 + i] = v.x;
                 yi[j1 * R0 + i] = v.y;
             }
@@ -496,9 +513,13 @@ __device__ __forceinline__ void glds16(const double2 *g, double2 *lds_base)
 /* points of the next row prefetched by k_row2<..., PRE>: 132 wave-instructions of 64 */
 constexpr int ROW_PRE_PTS = 8448;
 
-template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false>
+/* PF: the inputs of the next row's first 9-point group (55 % of a row at TPG = 768) are
+ * loaded into registers right after this row's first exchange, so their latency overlaps
+ * this row's remaining stages (needs the VGPRs of TPG = 768: 168 per thread) */
+template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
+    static_assert(PF == 0 || (F01 && !PRE), "PF prefetches fused01's first groups");
     using LS = List6<R0, R1, R2, R3, R4, R5>;
     constexpr int P = LS::P, NT = LS::Lloc(5) - 1; /* LDS twiddles tw[0, NT) */
     constexpr int NM0 = LS::template nmax<TPG>(), NMF = cdiv(P / (R0 * R1), TPG) * R0 * R1;
@@ -534,6 +555,8 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     __syncthreads();
     unsigned tp = (unsigned)__builtin_amdgcn_s_memrealtime();
     bool pre = false; /* PRE: this row's points [0, ROW_PRE_PTS) are in the image area */
+    double2 p0[(PF > 0 ? PF : 1) * R0 * R1]; /* PF: the next row's first PF groups of inputs */
+    if constexpr (PF > 0) f01_load0<R0, R1, P, TPG, PF>(p0, a.in + (long long)blockIdx.x * a.idist, jt0);
 #pragma unroll 1
     for (unsigned b = blockIdx.x; b < (unsigned)a.batch; b += gridDim.x) {
         int jt = jt0;
@@ -545,13 +568,17 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             if (PRE && pre)
                 fused01p<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, reinterpret_cast<const double2 *>(img), jt, sgn);
             else
-                fused01<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, img, jt, sgn);
+                fused01<R0, R1, P, TPG, CONJ, PF>(xr, xi, in, ltw, img, jt, sgn, p0);
             if (a.dbg) {
                 r8::pin(*reinterpret_cast<double(*)[8]>(xr));
                 mark(a, tp, 0); /* loads + stages 0-1 */
             }
             xchg1_f01<R0, R1, R2, P, TPG>(xr, img, jt);
             xchg1_f01<R0, R1, R2, P, TPG>(xi, img, jt);
+            if constexpr (PF > 0) { /* unconditional: the last row of a workgroup reloads itself */
+                const unsigned bn = b + gridDim.x < (unsigned)a.batch ? b + gridDim.x : b;
+                f01_load0<R0, R1, P, TPG, PF>(p0, a.in + (long long)bn * a.idist, jt);
+            }
             mark(a, tp, 1);
         } else {
             {
@@ -726,6 +753,29 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
                      : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, false> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, false>);
         if (rpre)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true, true>;
+        /* default: 512 threads (8 waves, 256 VGPRs per thread) with the next row's first input
+         * group (37 % of the row) loaded into registers during this row's stages 2-5: 113.5 ->
+         * 123.5 GSamples/s; HSFFT_ROW_T=1024 (16 waves, 128 VGPRs) / 768 (168 VGPRs) and
+         * HSFFT_ROW_PF=0/1/2 (groups prefetched) select the other variants */
+        const char *et = getenv("HSFFT_ROW_T"), *epf = getenv("HSFFT_ROW_PF");
+        const int rt = et ? atoi(et) : 512, rpf = epf ? atoi(epf) : (rt == 512 ? 1 : 0);
+        int threads = 1024;
+        if (f01 && !rpre && rt == 768) {
+            threads = 768;
+            fn = rpf ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 768, true, true, false, 1>
+                               : k_row2<3, 3, 5, 5, 7, 8, 768, false, true, false, 1>)
+                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 768, true, true> : k_row2<3, 3, 5, 5, 7, 8, 768, false, true>);
+        } else if (f01 && !rpre && rt == 512) { /* 8 waves, 256 VGPRs: room for 2 of 3 groups */
+            threads = 512;
+            fn = rpf >= 2 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 2>
+                                    : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 2>)
+               : rpf == 1 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
+                                    : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>)
+                          : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true> : k_row2<3, 3, 5, 5, 7, 8, 512, false, true>);
+        } else if (f01 && !rpre && rpf) {
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true, false, 1>
+                        : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true, false, 1>;
+        }
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));
         HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -739,7 +789,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
             a.dbg = s_dbg;
         }
         HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(1024), lds, st, a);
+        hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3((unsigned)threads), lds, st, a);
         HCHK(hipGetLastError());
         if (a.dbg) {
             static unsigned h[4096 * 8];
