@@ -698,15 +698,30 @@ __global__ __launch_bounds__(1024, 1) void k_r2c_walk(Args a, unsigned h, unsign
         return;
     }
     const unsigned j0 = s * T, j1 = min(j0 + T, B / 16);
+    /* HSFFT_R2C_DEBUG: per-workgroup phase clock in a.laux (thread 0, 100 MHz ticks):
+     * [0] twiddles + stages (incl. the data wait), [1] image write + barrier, [2] pairs + stores */
+    unsigned *dbg = (unsigned *)a.laux, tp = 0;
+#define R2CW_MARK(i)                                                              \
+    if (dbg && tid == 0) {                                                        \
+        const unsigned tn = (unsigned)__builtin_amdgcn_s_memrealtime();           \
+        dbg[blockIdx.x * 4 + (i)] += tn - tp;                                     \
+        tp = tn;                                                                  \
+    }
+    if (dbg && tid == 0) tp = (unsigned)__builtin_amdgcn_s_memrealtime();
     r2cw_load(xr, xi, row, B, half ? B - 8 * j0 - 8 : 8 * j0 + 1, t);
 #pragma unroll 1
     for (unsigned j = j0; j < j1; j++) {
         const unsigned q0 = half ? B - 8 * j - 8 : 8 * j + 1;
         r2cw_tile<SGN>(xr, xi, B, q0, a.tw, img, ltw, t);
+        if (dbg) {
+            r8::pin(xr);
+            R2CW_MARK(0)
+        }
         /* the last exchange ended with a barrier: both images are free */
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) img[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
         __syncthreads();
+        R2CW_MARK(1)
         /* the next tile's points load while this tile's pairs are formed and stored (the pair
          * loop reads this tile's points back from the image) */
         {   /* unconditional (the last tile reloads itself): a branch around the loads makes the
@@ -746,7 +761,10 @@ __global__ __launch_bounds__(1024, 1) void k_r2c_walk(Args a, unsigned h, unsign
                 }
             }
         }
+        R2CW_MARK(2)
+        if (dbg && tid == 0) dbg[blockIdx.x * 4 + 3] += 1;
     }
+#undef R2CW_MARK
     /* the carry of the last tile: bin 8*j1 of the off-line streams (already written by the
      * other stream's aligned stores when j1 is the row's last tile: column B/2) */
     if (j1 < B / 16 && j1 > j0) {
@@ -755,6 +773,165 @@ __global__ __launch_bounds__(1024, 1) void k_r2c_walk(Args a, unsigned h, unsign
             const unsigned u = jt + jj * TPG;
             if (!half && g == 0) X[u * B + 8 * j1] = cry[u];
             if (half && g == 7) X[h + (P - 1 - u) * B + 8 * j1] = cry[u];
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ r2c split, 512-thread walk
+ * k_r2c_walk's whole-line stores with k_r2c_fused's sequential hi / lo tiles, in ONE 8-wave
+ * workgroup per CU with 256 VGPRs, software pipelined instead of relying on a second resident
+ * workgroup: the lo tile's points and twiddle runs load while the hi tile is transformed, the
+ * next hi tile's while the lo tile is transformed (two register buffers A / B, transformed in
+ * place).  The lo thread writes all four streams of its pair; X[k] and X[h+k] go out on whole
+ * lines through the one-lane shift and the carried entry (LDS, same thread), as in k_r2c_walk. */
+struct R2cBuf {
+    double r[8], i[8];
+    double2 w[7]; /* stage-2 twiddle run, coalesced order (redistributed when used) */
+    double2 l;    /* this thread's entry of the stage-0/1 twiddle runs (threads < 504) */
+};
+
+__device__ __forceinline__ void r2cw2_issue(R2cBuf &d, const double2 *row, unsigned B, unsigned q0, const double2 *tw,
+                                            unsigned tid)
+{
+    constexpr int TPG = 64;
+    const unsigned lane0 = ((tid >> 3) * B + q0 + (tid & 7)) * 16u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
+        d.r[i] = v.x;
+        d.i[i] = v.y;
+    }
+    r8::Args ta;
+    ta.tw = tw;
+    ta.B = B;
+    r8::load_tw_co<64>(d.w, ta, (int)(tid >> 3), q0);
+    const unsigned t = tid < 504 ? tid : 0, r = t / 56, e = t % 56;
+    const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
+    d.l = tw[src];
+}
+
+/* twiddles of the buffered tile -> ltw (runs) and w2 (redistributed through the image) */
+__device__ __forceinline__ void r2cw2_tw(const R2cBuf &d, double2 (&w2)[7], double2 *lds, double2 *ltw, unsigned tid)
+{
+#pragma unroll
+    for (int i = 0; i < 7; i++) w2[i] = d.w[i];
+    __syncthreads(); /* earlier readers of the image and of ltw are done */
+    if (tid < 504) ltw[tid] = d.l;
+    r8::redistribute_tw(w2, lds);
+    __syncthreads();
+}
+
+constexpr int R2CW2_LDS = (512 * 8 + 504 + 1024) * 16;
+
+template <int SGN>
+__global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsigned T, unsigned W)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    double2 *ltw = lds + P * G, *cry = ltw + 504;
+    double *ld = reinterpret_cast<double *>(lds); /* [0, 4096): split image / hi imag, [4096, 8192): hi real */
+    /* a.tile_major: consecutive blocks (one XCD) take the same walk segment of consecutive rows,
+     * so the segment's twiddle runs and twiddle2 slice are read from that XCD's L2 */
+    const unsigned blk = xcd_remap(blockIdx.x), nb = (unsigned)a.batch;
+    const unsigned b = a.tile_major ? blk % nb : blk / (W + 1), s = a.tile_major ? blk / nb : blk % (W + 1);
+    const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
+    const double2 *row = a.in + (long long)b * a.idist;
+    double2 *X = a.out + (long long)b * a.odist;
+    const double2 *w2t = a.saux;
+    if (s == W) { /* column 0 (k = u*B pairs with (P-u)*B), as k_r2c_fused */
+        const unsigned g = tid0 & 7, jt = tid0 >> 3;
+        double xr[8], xi[8];
+        double2 w2[7];
+        r2c_load(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
+        r2c_stages<SGN, false>(xr, xi, w2, lds, ltw, tid0);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B;
+            const double2 zk = make_double2(xr[jj], xi[jj]);
+            if (u == 0) {
+                X[0] = make_double2(zk.x + zk.y, 0.0);
+                X[h] = make_double2(zk.x - zk.y, 0.0);
+            } else {
+                const double2 zh = lds[(P - u) * G];
+                double re, im;
+                r8::r2c_pair(zk, zh, w2t[k], re, im);
+                X[k] = make_double2(re, im);
+                X[N - k] = make_double2(re, -im);
+            }
+        }
+        return;
+    }
+    const unsigned j0 = s * T, j1 = min(j0 + T, B / 16);
+    R2cBuf A, Bf;
+    r2cw2_issue(A, row, B, B - 8 * j0 - 8, a.tw, tid0); /* hi(j0) */
+#pragma unroll 1
+    for (unsigned j = j0; j < j1; j++) {
+        unsigned tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const unsigned g = tid & 7, jt = tid >> 3;
+        const unsigned qlo = 8 * j + 1;
+        r2cw2_issue(Bf, row, B, qlo, a.tw, tid); /* lo(j) loads while hi(j) is transformed */
+        double2 w2[7];
+        /* ---- hi(j), in place in A */
+        r2cw2_tw(A, w2, lds, ltw, tid);
+        r2c_stages<SGN, false>(A.r, A.i, w2, lds, ltw, tid);
+        double him[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) him[jj] = A.i[jj];
+        /* ---- lo(j), in place in Bf */
+        r2cw2_tw(Bf, w2, lds, ltw, tid);
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) ld[4096 + (jt + jj * TPG) * G + g] = A.r[jj]; /* hi real parts wait here */
+        {   /* hi(j+1) loads while lo(j) is transformed; unconditional (the last tile reloads) */
+            const unsigned jn = j + 1 < j1 ? j + 1 : j;
+            r2cw2_issue(A, row, B, B - 8 * jn - 8, a.tw, tid);
+        }
+        r2c_stages<SGN, true>(Bf.r, Bf.i, w2, lds, ltw, tid);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
+        __syncthreads();
+        /* ---- pairs: X[N-k], X[h-k] aligned; X[k], X[h+k] shifted one lane onto line [8j, 8j+8) */
+        const bool first = j == j0;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B + qlo + g, hk = h - k;
+            const unsigned sl = (P - 1 - u) * G + (7 - g);
+            const double2 zk = make_double2(Bf.r[jj], Bf.i[jj]), zh = make_double2(ld[4096 + sl], ld[sl]);
+            double re, im, re2, im2;
+            r8::r2c_pair(zk, zh, w2t[k], re, im);
+            r8::r2c_pair(zh, zk, w2t[hk], re2, im2);
+            X[N - k] = make_double2(re, -im);
+            X[hk] = make_double2(re2, im2);
+            const double2 va = grp_shift<-1>(make_double2(re, im)), vb = grp_shift<-1>(make_double2(re2, -im2));
+            const unsigned p = u * B + 8 * j + g;
+            if (g != 0) {
+                X[p] = va;
+                X[h + p] = vb;
+            } else {
+                if (!first) {
+                    X[p] = cry[u];
+                    X[h + p] = cry[512 + u];
+                }
+                cry[u] = va;
+                cry[512 + u] = vb;
+            }
+        }
+    }
+    /* the last tile's carries (bin 8*j1 of X[k] / X[h+k]; at the row's last tile column B/2,
+     * already written by the aligned streams) */
+    if (j1 < B / 16 && j1 > j0 && (tid0 & 7) == 0) {
+        const unsigned jt = tid0 >> 3;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, p = u * B + 8 * j1;
+            X[p] = cry[u];
+            X[h + p] = cry[512 + u];
         }
     }
 }
@@ -780,14 +957,47 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     a.tiles = a.tiles_q = B / 16 + 1;
     /* whole-line tile walk (opt-in, HSFFT_R2C_WALK=1): bit-exact, but one 1024-thread workgroup
      * per CU loses more overlap than the aligned stores gain (c5 95.4 vs 98.2 GSamples/s) */
-    if (!compact && env("HSFFT_R2C_WALK", 0) && !getenv("HSFFT_R2C_PROBE")) {
+    /* default: k_r2c_walk2, 32 tile pairs per walk (c5 98.4 -> 100.6-101.4 GSamples/s);
+     * HSFFT_R2C_WALK=0: k_r2c_fused, =1: k_r2c_walk */
+    const int walk = env("HSFFT_R2C_WALK", 2);
+    if (!compact && walk == 2 && !getenv("HSFFT_R2C_PROBE")) { /* 512-thread walk */
+        const long long T = env("HSFFT_R2C_WT", 32) > 0 ? env("HSFFT_R2C_WT", 32) : 32, W = (B / 16 + T - 1) / T;
+        const long long grid = (W + 1) * (long long)batch;
+        if (grid <= 0 || grid > 0x7fffffffLL) return -1;
+        void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk2<1> : k_r2c_walk2<-1>;
+        a.tile_major = env("HSFFT_R2C_ORDER", 0); /* measured 87-93 vs 101: the rows' DRAM pages matter more */
+        HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW2_LDS));
+        hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), R2CW2_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
+        HCHK(hipGetLastError());
+        return 0;
+    }
+    if (!compact && walk == 1 && !getenv("HSFFT_R2C_PROBE")) {
         const long long T = env("HSFFT_R2C_WT", 16) > 0 ? env("HSFFT_R2C_WT", 16) : 16, W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
         void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk<1> : k_r2c_walk<-1>;
         HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW_LDS));
+        static unsigned *s_dbg = nullptr;
+        const bool dbg = env("HSFFT_R2C_DEBUG", 0) && grid <= (1 << 20);
+        if (dbg) {
+            if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, (size_t)(1 << 20) * 4 * sizeof(unsigned)));
+            HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 4 * sizeof(unsigned), st));
+            a.laux = (const double2 *)s_dbg;
+        }
         hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(1024), R2CW_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());
+        if (dbg) {
+            unsigned *hb = (unsigned *)malloc((size_t)grid * 4 * sizeof(unsigned));
+            HCHK(hipStreamSynchronize(st));
+            HCHK(hipMemcpy(hb, s_dbg, (size_t)grid * 4 * sizeof(unsigned), hipMemcpyDeviceToHost));
+            double ph[4] = {0, 0, 0, 0};
+            for (long long i = 0; i < grid; i++)
+                for (int k = 0; k < 4; k++) ph[k] += hb[i * 4 + k];
+            free(hb);
+            const double n = ph[3] > 0 ? ph[3] : 1;
+            fprintf(stderr, "k_r2c_walk per tile pair (us): twiddles+stages %.2f  image+barrier %.2f  pairs+stores %.2f | steps %.0f\n",
+                    ph[0] / n / 100, ph[1] / n / 100, ph[2] / n / 100, n);
+        }
         return 0;
     }
     const long long grid = a.tiles * (long long)batch;

@@ -448,7 +448,7 @@ def test_two_pass_2pow21_batched():
 @pytest.mark.parametrize("fuse", ["0", "1", "2"])
 @pytest.mark.parametrize("n,sgn", [(1 << 19, 1), (1 << 22, 1), (1 << 22, -1), (1 << 13, 1)])
 def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
-    """the real.c split fused into the last c2c pass (HSFFT_R2C_FUSE=1, default: pf::k_r2c_fused;
+    """the real.c split fused into the last c2c pass (HSFFT_R2C_FUSE=1, default: pf::k_r2c_walk2;
     2: r8::k_r2c_last; 0: separate split kernel), bit-exact, both plan signs, odd batch."""
     monkeypatch.setenv("HSFFT_R2C_FUSE", fuse)
     x = T.real_input(n, 23, batch=3).reshape(3, n)
@@ -461,7 +461,7 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wt", ["16", "1", "5", "4096", "walk0"])
+@pytest.mark.parametrize("wt", ["16", "1", "5", "4096", "walk0", "w2:16", "w2:1", "w2:5", "w2:4096"])
 @pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
 def test_r2c_walk(n, sgn, wt, monkeypatch):
     """pf::k_r2c_walk (opt-in split kernel of the reference-layout r2c): walks of WT tile pairs
@@ -471,6 +471,9 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
     one-tile-per-workgroup k_r2c_fused.  Bit-exact vs the oracle, odd batch."""
     if wt == "walk0":
         monkeypatch.setenv("HSFFT_R2C_WALK", "0")
+    elif wt.startswith("w2:"):
+        monkeypatch.setenv("HSFFT_R2C_WALK", "2")
+        monkeypatch.setenv("HSFFT_R2C_WT", wt[3:])
     else:
         monkeypatch.setenv("HSFFT_R2C_WALK", "1")
         monkeypatch.setenv("HSFFT_R2C_WT", wt)
