@@ -550,7 +550,7 @@ int grid_for(long long n, int threads)
 #include "hsfft_pass_wl.h"
 #include "hsfft_pass_mr.h"
 #include "hsfft_fused.h"
-#include "hsfft_fused2.h"
+#include "hsfft_fused2.h" /* constants and arguments; kernels in hsfft_device_fz2.hip */
 #include "hsfft_blue_pf.h"
 #include "hsfft_blue_xcd.h"
 
@@ -772,6 +772,9 @@ int hsd_fused20(const void *in, long long idist, void *out, long long odist, con
 /* fixed-role fused 2^20 launch (hsfft_fused2.h): counter block of 128-B lines -- [8] the sticky
  * error word (checked by hsd_sync), line 1..8 ticket heads, then per row one line of pass-A
  * items done and one line of pass-B tiles done */
+extern "C" int hsd_fz2_launch(const fz2::F2Args *a, int sgn, int conj, int plain, int nt, hipStream_t st, char *err,
+                              size_t errlen);
+
 int hsd_fused20b(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
                  int conj, int na, int nb, int lag, int spin_max)
 {
@@ -828,11 +831,12 @@ int hsd_fused20b(const void *in, long long idist, void *out, long long odist, co
         HCHK(hipMemsetAsync(s_dbg2, 0, (size_t)(na + nb) * 8 * sizeof(unsigned), stream()));
         a.dbg = s_dbg2;
     }
-    fz2::ffn fn = fz2::fused2_fn(sgn, conj, conj ? 0 : (getenv("HSFFT_FZ2_PLAIN") ? atoi(getenv("HSFFT_FZ2_PLAIN")) & 3 : 0),
-                                 getenv("HSFFT_FZ2_NT") ? atoi(getenv("HSFFT_FZ2_NT")) & 3 : 0);
-    HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fz2::LDS_BYTES));
-    hipLaunchKernelGGL(fn, dim3((unsigned)(na + nb)), dim3(512), fz2::LDS_BYTES, stream(), a);
-    HCHK(hipGetLastError());
+    {
+        const int plain = conj ? 0 : (getenv("HSFFT_FZ2_PLAIN") ? atoi(getenv("HSFFT_FZ2_PLAIN")) & 3 : 0);
+        const int nt = getenv("HSFFT_FZ2_NT") ? atoi(getenv("HSFFT_FZ2_NT")) & 3 : 0;
+        const int rc = hsd_fz2_launch(&a, sgn, conj, plain, nt, stream(), g_err, sizeof g_err);
+        if (rc) return rc;
+    }
     HCHK(hipMemcpyAsync(g_fz_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
     if (dbg) { /* per role: mean items, wait and work per item (us), span of first start .. last end */
         static unsigned h[4096 * 8];

@@ -58,6 +58,13 @@ struct F2Args {
     unsigned *dbg;   /* optional per-workgroup trace (8 words): items, busy, wait, first, last */
 };
 
+constexpr size_t LDS_BYTES = (4096 + 504) * sizeof(double2) + 16;
+
+/* The kernels below are compiled in their own translation unit (hsfft_device_fz2.hip, which
+ * defines HSFFT_FZ2_KERNELS): instantiated next to the production passes in
+ * hsfft_device.hip, they changed the register allocation of pf::k_firstq<4,3,2> (128 VGPRs
+ * + 4 dwords of spill instead of none). */
+#ifdef HSFFT_FZ2_KERNELS
 __device__ __forceinline__ unsigned now32() { return (unsigned)__builtin_amdgcn_s_memrealtime(); }
 
 /* polling pause: `n` x s_sleep 4 (~4 x 64 clocks each) */
@@ -264,6 +271,6 @@ inline ffn fused2_fn(int sgn, int conj, int plain = 0, int nt = 0)
     return conj ? k_fused2<-1, true> : k_fused2<-1, false>;
 }
 
-constexpr size_t LDS_BYTES = (4096 + 504) * sizeof(double2) + 16;
+#endif /* HSFFT_FZ2_KERNELS */
 
 }  // namespace fz2
