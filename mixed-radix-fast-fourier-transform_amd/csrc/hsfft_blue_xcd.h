@@ -27,7 +27,7 @@
  * pass) and the tile's forward runs (P2; conjugated for P3) in LDS, the tile's stage-2
  * twiddles in registers.
  *
- * Hand-off (MI355X_MICROARCH.md visibility table, row 1; as hsfft_fused2.h): images are
+ * Hand-off (MI355X_MICROARCH.md visibility table, row 1): images are
  * written with sc1 stores, every wave waits vmcnt(0), a workgroup barrier, one lane adds 1
  * (relaxed, agent scope) to the group's counter; waiters poll it (relaxed agent loads, bounded
  * by a ~10 s real-time deadline that sets the sticky error word), join a barrier and read the
@@ -40,6 +40,8 @@
 #pragma once
 
 namespace bxc {
+
+constexpr unsigned long long T_LIMIT = 1ull << 30; /* bounded waits: ~10 s of the 100 MHz real-time counter */
 
 constexpr unsigned NTILE = 64;  /* 8-column tiles of the 512 x 512 image = workgroups per group */
 constexpr unsigned CS = 32;     /* counter stride (128-B line per counter) */
@@ -99,7 +101,7 @@ __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned targ
         unsigned bad = 0;
         while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             for (unsigned k = 0; k < a.sleep; k++) __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > fz2::T_LIMIT ||
+            if (__builtin_amdgcn_s_memrealtime() - t0 > T_LIMIT ||
                 __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 bad = 1;

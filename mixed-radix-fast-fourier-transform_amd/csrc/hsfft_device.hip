@@ -550,7 +550,6 @@ int grid_for(long long n, int threads)
 #include "hsfft_pass_wl.h"
 #include "hsfft_pass_mr.h"
 #include "hsfft_fused.h"
-#include "hsfft_fused2.h" /* constants and arguments; kernels in hsfft_device_fz2.hip */
 #include "hsfft_blue_pf.h"
 #include "hsfft_blue_xcd.h"
 
@@ -764,103 +763,6 @@ int hsd_fused20(const void *in, long long idist, void *out, long long odist, con
             fprintf(stderr, "           A phases (us): load %.2f compute %.2f store-drain %.2f | ticket %.2f per item\n",
                     na ? pl / 100.0 / na : 0.0, na ? pc / 100.0 / na : 0.0, na ? ps / 100.0 / na : 0.0,
                     tk ? pt / 100.0 / tk : 0.0);
-        }
-    }
-    return 0;
-}
-
-/* fixed-role fused 2^20 launch (hsfft_fused2.h): counter block of 128-B lines -- [8] the sticky
- * error word (checked by hsd_sync), line 1..8 ticket heads, then per row one line of pass-A
- * items done and one line of pass-B tiles done */
-extern "C" int hsd_fz2_launch(const fz2::F2Args *a, int sgn, int conj, int plain, int nt, hipStream_t st, char *err,
-                              size_t errlen);
-
-int hsd_fused20b(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
-                 int conj, int na, int nb, int lag, int spin_max)
-{
-    int dev = 0;
-    HCHK(hipGetDevice(&dev));
-    if (dev < 0 || dev >= HS_MAX_DEV) return -1;
-    if (batch < 1 || (sgn != 1 && sgn != -1) || na < 1 || nb < 1 || nb > (int)fz2::QT) {
-        snprintf(g_err, sizeof g_err, "hsd_fused20b: unsupported geometry (batch=%d na=%d nb=%d)", batch, na, nb);
-        return -1;
-    }
-    const size_t CS = fz2::CS;
-    const size_t need = (CS * (1 + fz2::NQ) + 2 * CS * (size_t)batch) * sizeof(unsigned);
-    if (g_fz_bytes[dev] < need) {
-        if (g_fz_ctr[dev]) {
-            HCHK(hipStreamSynchronize(stream()));
-            HCHK(hipFree(g_fz_ctr[dev]));
-        }
-        const size_t alloc = (need + 4095) & ~(size_t)4095;
-        HCHK(hipMalloc((void **)&g_fz_ctr[dev], alloc));
-        HCHK(hipMemset(g_fz_ctr[dev], 0, alloc));
-        g_fz_bytes[dev] = alloc;
-        if (!g_fz_err_host[dev]) {
-            HCHK(hipHostMalloc((void **)&g_fz_err_host[dev], 64, hipHostMallocDefault));
-            *g_fz_err_host[dev] = 0;
-        }
-    }
-    unsigned *ctr = g_fz_ctr[dev];
-    HCHK(hipMemsetAsync(ctr + CS, 0, (CS * fz2::NQ + 2 * CS * (size_t)batch) * sizeof(unsigned), stream()));
-    fz2::F2Args a;
-    a.in = (const double2 *)in;
-    a.out = (double2 *)out;
-    a.tw = (const double2 *)tw;
-    a.idist = idist;
-    a.odist = odist;
-    a.head = ctr + CS;
-    a.err = ctr + 8;
-    a.adone = ctr + CS * (1 + fz2::NQ);
-    a.bdone = a.adone + CS * (size_t)batch;
-    a.batch = (unsigned)batch;
-    a.na = (unsigned)na;
-    a.nb = (unsigned)nb;
-    a.lag = (unsigned)(lag < 1 ? 1 : lag);
-    a.spin_max = (unsigned)(spin_max < 0 ? 0 : spin_max);
-    {
-        const char *e = getenv("HSFFT_FZ_SLEEP");
-        a.sleep = e ? (unsigned)atoi(e) : 2u;
-    }
-    a.dbg = nullptr;
-    static unsigned *s_dbg2 = nullptr;
-    const char *dbgenv = getenv("HSFFT_FZ_DEBUG");
-    const bool dbg = dbgenv && atoi(dbgenv) && na + nb <= 4096;
-    if (dbg) {
-        if (!s_dbg2) HCHK(hipMalloc((void **)&s_dbg2, 4096 * 8 * sizeof(unsigned)));
-        HCHK(hipMemsetAsync(s_dbg2, 0, (size_t)(na + nb) * 8 * sizeof(unsigned), stream()));
-        a.dbg = s_dbg2;
-    }
-    {
-        const int plain = conj ? 0 : (getenv("HSFFT_FZ2_PLAIN") ? atoi(getenv("HSFFT_FZ2_PLAIN")) & 3 : 0);
-        const int nt = getenv("HSFFT_FZ2_NT") ? atoi(getenv("HSFFT_FZ2_NT")) & 3 : 0;
-        const int rc = hsd_fz2_launch(&a, sgn, conj, plain, nt, stream(), g_err, sizeof g_err);
-        if (rc) return rc;
-    }
-    HCHK(hipMemcpyAsync(g_fz_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
-    if (dbg) { /* per role: mean items, wait and work per item (us), span of first start .. last end */
-        static unsigned h[4096 * 8];
-        HCHK(hipStreamSynchronize(stream()));
-        HCHK(hipMemcpy(h, s_dbg2, (size_t)(na + nb) * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
-        for (int role = 0; role < 2; role++) {
-            const int b0 = role ? na : 0, b1 = role ? na + nb : na;
-            double it = 0, wt = 0, wk = 0;
-            unsigned first = 0xffffffffu, last = 0, mn = 0xffffffffu, mx = 0;
-            for (int b = b0; b < b1; b++) {
-                const unsigned *d = h + b * 8;
-                it += d[0];
-                wt += d[1];
-                wk += d[2];
-                if (d[0]) {
-                    first = d[3] < first ? d[3] : first;
-                    last = d[4] > last ? d[4] : last;
-                    mn = d[0] < mn ? d[0] : mn;
-                    mx = d[0] > mx ? d[0] : mx;
-                }
-            }
-            fprintf(stderr, "fz2 %s: wgs %d items %.0f (per wg %u..%u) wait/item %.2f us work/item %.2f us span %.2f ms\n",
-                    role ? "B" : "A", b1 - b0, it, mn, mx, it ? wt / it / 100.0 : 0.0, it ? wk / it / 100.0 : 0.0,
-                    (last - first) / 1e5);
         }
     }
     return 0;

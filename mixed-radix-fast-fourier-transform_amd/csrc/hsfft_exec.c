@@ -717,14 +717,6 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     }
     if (n == 1)
         return launch_pass(e, ds, 0, I, idist, O, odist, batch, sgn, conj, dir, load_op, laux, store_op, saux, nsig);
-    if (fused20_ok(e, odist, batch, load_op, store_op) && env_int("HSFFT_FUSED", 0) == 2) {
-        /* fixed-role fused launch (hsfft_fused2.h) */
-        const int ncu = hsd_cu_count() > 0 ? hsd_cu_count() : 256;
-        int rc = hsd_fused20b(I, idist, O, odist, ds->d_tw, batch, sgn, conj, env_int("HSFFT_FZ2_NA", ncu),
-                              env_int("HSFFT_FZ2_NB", 256), env_int("HSFFT_FZ_LAG", 3), env_int("HSFFT_FZ_SPIN", 4096));
-        if (rc) hs_seterr("fused pass: %s", hsd_errstr());
-        return rc;
-    }
     if (fused20_ok(e, odist, batch, load_op, store_op)) {
         const int R = fused_rows(batch);
         int grid = env_int("HSFFT_FZ_GRID", 0);

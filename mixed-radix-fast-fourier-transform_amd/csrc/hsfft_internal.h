@@ -131,12 +131,6 @@ int hsd_copy_rows(const void *src, long long sdist, long long soff, long long nc
 /* 2^20 = [4,8,8,8 | 8,8,8] as one persistent launch (hsfft_fused.h); rows of 2^20 complex */
 int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
                 int conj, int rows_per_group, int lag, int grid);
-/* the same with fixed workgroup roles (hsfft_fused2.h): na pass-A, nb pass-B workgroups */
-/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h); 1 = not applicable */
-int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
-                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng);
-int hsd_fused20b(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
-                 int conj, int na, int nb, int lag, int spin_max);
 int hsd_cu_count(void);
 
 /* timing on the library stream */

@@ -450,7 +450,6 @@ __device__ __forceinline__ void tile888(double (&xr)[8], double (&xi)[8], const 
  * sign -sgn; :1838-1855) on the same registers: column q of the former is column m = q of
  * the latter and thread jt holds points u = jt + 64*i of both, so the intermediate never
  * goes back to HBM.  a.sgn/a.conj: forward FFT; sgn2/conj2: inverse FFT; a.saux = hk. */
-#ifndef HSFFT_SECOND_TU /* plain kernels: defined once, in hsfft_device.hip */
 __global__ __launch_bounds__(512) void k_blue_mid(Args a, int sgn2, int conj2)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -497,9 +496,6 @@ __global__ __launch_bounds__(512) void k_blue_mid(Args a, int sgn2, int conj2)
 #pragma unroll
     for (int jj = 0; jj < 8; jj++) out[q * P + jt + jj * TPG] = make_double2(xr[jj], xi[jj]);
 }
-#else
-__global__ __launch_bounds__(512) void k_blue_mid(Args a, int sgn2, int conj2);
-#endif
 
 inline int launch_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch,
                            int sgn, int conj, int dir, int sgn2, int conj2, hipStream_t st)
@@ -539,7 +535,6 @@ __device__ __forceinline__ void r2c_pair(double2 a, double2 c, double2 w, double
     im = (a.y - c.y + (t2 * w.x) - (t1 * w.y)) / 2.0;
 }
 
-#ifndef HSFFT_SECOND_TU /* plain kernels: defined once, in hsfft_device.hip */
 __global__ __launch_bounds__(512, 4) void k_r2c_last(Args a, long long h)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -604,9 +599,6 @@ __global__ __launch_bounds__(512, 4) void k_r2c_last(Args a, long long h)
         }
     }
 }
-#else
-__global__ __launch_bounds__(512, 4) void k_r2c_last(Args a, long long h);
-#endif
 
 inline int launch_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2,
                            long long h, long long B, int batch, int sgn, hipStream_t st)

@@ -228,13 +228,6 @@ int hsd_fused20(const void *in, long long idist, void *out, long long odist, con
     touch_rows_w(out, odist, 1 << 20, batch, 16);
     return 0;
 }
-int hsd_fused20b(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
-                 int conj, int na, int nb, int lag, int spin_max)
-{
-    touch_rows_r(in, idist, 1 << 20, batch, 16);
-    touch_rows_w(out, odist, 1 << 20, batch, 16);
-    return 0;
-}
 int hsd_timer_start(void) { return 0; }
 int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *ms)
 {

@@ -116,23 +116,7 @@ def test_fused_bit_exact(batch, r, lag, monkeypatch):
         assert T.bits_equal(y, ref), (batch, r, lag, sgn, T.mismatches(y, ref))
 
 
-@pytest.mark.parametrize("batch,na,nb,lag", [(1, 256, 256, 3), (2, 256, 256, 1), (7, 256, 256, 3), (5, 64, 256, 2),
-                                             (3, 256, 128, 3), (4, 40, 100, 9)])
-def test_fused_roles_bit_exact(batch, na, nb, lag, monkeypatch):
-    """fixed-role fused launch (hsfft_fused2.h): pass-A / pass-B workgroup counts, odd
-    batches, B workgroups owning more than one q-tile, both signs, bit-exact vs the oracle"""
-    monkeypatch.setenv("HSFFT_FUSED", "2")
-    monkeypatch.setenv("HSFFT_FZ2_NA", str(na))
-    monkeypatch.setenv("HSFFT_FZ2_NB", str(nb))
-    monkeypatch.setenv("HSFFT_FZ_LAG", str(lag))
-    x = T.complex_input(N, 0xF2D0 ^ batch, batch=batch).reshape(batch, N)
-    for sgn in (1, -1):
-        y = _run(x, sgn)
-        ref = _oracle(x, sgn, ("f2", batch))
-        assert T.bits_equal(y, ref), (batch, na, nb, lag, sgn, T.mismatches(y, ref))
-
-
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1"])
 def test_fused_large_batch_vs_two_launch(mode, monkeypatch):
     """64 rows (16 GiB of pass traffic): the fused launch equals the two-launch path bit for
     bit on every row and the oracle on sampled rows; no dependency wait timed out."""
