@@ -1,0 +1,69 @@
+"""Register budgets of the default hot-path kernels, read from the gfx950 code object inside
+lib/libhsfft.so (no GPU needed).
+
+Why a test: in round 2 an opt-in experiment compiled into the same translation unit changed
+the register allocation of the 2^20 first pass (pf::k_firstq<4,3,2>: 4 dwords of scratch spill
+that round 1 did not have, pass A 24.0 -> 24.8 ms) without any change to its source.  Spills
+in these kernels cost time, so a spill appearing in one of them is a regression to look at
+(DESIGN.md §5).  The known, intrinsic spill of the persistent Bluestein kernel is capped at
+its measured value.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "mixed-radix-fast-fourier-transform_amd", "lib", "libhsfft.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+# (kernel-name regex on the mangled name, max VGPR spill dwords)
+BUDGETS = [
+    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]ELb0E", 0),  # 2^20 pass A (c2)
+    (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]ELb0E", 0),  # 2^20 pass B (c2)
+    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]ELb0E", 0),  # 2^21 pass A (c5)
+    (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0),  # r2c split (c5)
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1E", 0),  # 12600 row (c3)
+    (r"^_ZN3bxc6k_bxcdILin?1ELb0E", 8),  # persistent Bluestein (c4): 8 dwords, intrinsic
+]
+
+
+def _metadata():
+    if not os.path.exists(LIB):
+        pytest.skip("lib/libhsfft.so not built")
+    bundler, readelf = os.path.join(LLVM, "clang-offload-bundler"), os.path.join(LLVM, "llvm-readelf")
+    if not (os.path.exists(bundler) and os.path.exists(readelf) and shutil.which("objcopy")):
+        pytest.skip("ROCm LLVM tools / objcopy not available")
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    fat, co = os.path.join(tmp, f"hsfft_fat_{os.getpid()}.bin"), os.path.join(tmp, f"hsfft_co_{os.getpid()}.o")
+    try:
+        subprocess.check_call(["objcopy", f"--dump-section=.hip_fatbin={fat}", LIB])
+        subprocess.check_call([bundler, "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
+                               f"--output={co}", "--unbundle"])
+        notes = subprocess.check_output([readelf, "--notes", co], text=True)
+    finally:
+        for f in (fat, co):
+            if os.path.exists(f):
+                os.remove(f)
+    kernels, cur = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s+\.name:\s+(\S+)", line)
+        if m:
+            cur = m.group(1)
+            kernels.setdefault(cur, {})
+            continue
+        m = re.match(r"\s+\.(vgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\d+)", line)
+        if m and cur:
+            kernels[cur][m.group(1)] = int(m.group(2))
+    return kernels
+
+
+def test_hot_kernels_do_not_spill():
+    kernels = _metadata()
+    for pat, cap in BUDGETS:
+        hits = {k: v for k, v in kernels.items() if re.match(pat, k)}
+        assert hits, f"no kernel matches {pat}"
+        for name, res in hits.items():
+            assert res.get("vgpr_spill_count", 0) <= cap, (name, res)  # SGPR spills go to VGPR lanes: cheap
