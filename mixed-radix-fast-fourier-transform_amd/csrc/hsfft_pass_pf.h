@@ -231,13 +231,8 @@ __device__ __forceinline__ double pair_swap(double v)
     return r;
 }
 
-/* PF (opt-in, HSFFT_PFQ_PF=1): one workgroup per CU with 256 VGPRs, the next column group's
- * loads issued before the current group is transformed (software pipelined instead of a second
- * resident workgroup).  Bit-exact; measured slower -- 2^20 pass A 27.2-28.7 vs 24.9 ms, c5
- * 92-94 vs 97.9 GSamples/s: the pass is bound by its row-segment request stream, not by load
- * latency, and one workgroup per CU halves the requests in flight */
-template <int R0, int N8, int G, int SGN, bool CONJ, bool PF = false>
-__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), PF ? 2 : 4) void k_firstq(Args a)
+template <int R0, int N8, int G, int SGN, bool CONJ>
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
 {
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG, NT = TPG * G, NB = 8 / R0, S0 = P / R0;
@@ -272,8 +267,6 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), PF ? 2 : 4) void k_firstq
                 vb[c * R0 + i] = ldg(rb, offB);
             }
     };
-    double2 pa[8], pb[8];
-    if constexpr (PF) load_group(pa, pb, 0, threadIdx.x);
 #pragma unroll 1
     for (int it = 0; it < nit; it++) {
         unsigned tid = threadIdx.x;
@@ -281,17 +274,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), PF ? 2 : 4) void k_firstq
         const unsigned h = tid % G, jt = tid / G, odd = jt & 1;
         const unsigned m0 = (sg + it * groups) * (2 * G);
         double2 va[8], vb[8];
-        if constexpr (PF) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                va[k] = pa[k];
-                vb[k] = pb[k];
-            }
-            /* unconditional (the last group reloads itself): no branch around the loads */
-            load_group(pa, pb, it + 1 < nit ? it + 1 : it, tid);
-        } else {
-            load_group(va, vb, it, tid);
-        }
+        load_group(va, vb, it, tid);
         double xr[8], xi[8], yr[8], yi[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -1077,10 +1060,6 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = q;
             *threads = 512;
             *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
-            if (env("HSFFT_PFQ_PF", 0)) {
-                if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 2, 1, true, true> : k_firstq<4, 3, 2, 1, false, true>;
-                return l->conj ? k_firstq<4, 3, 2, -1, true, true> : k_firstq<4, 3, 2, -1, false, true>;
-            }
             if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 2, 1, true> : k_firstq<4, 3, 2, 1, false>;
             return l->conj ? k_firstq<4, 3, 2, -1, true> : k_firstq<4, 3, 2, -1, false>;
         }
@@ -1111,10 +1090,6 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = q;
             *threads = 512;
             *lds = (size_t)4096 * sizeof(double) + 511 * sizeof(double2);
-            if (env("HSFFT_PFQ_PF", 0)) {
-                if (l->sgn == 1) return l->conj ? k_firstq<8, 3, 1, 1, true, true> : k_firstq<8, 3, 1, 1, false, true>;
-                return l->conj ? k_firstq<8, 3, 1, -1, true, true> : k_firstq<8, 3, 1, -1, false, true>;
-            }
             if (l->sgn == 1) return l->conj ? k_firstq<8, 3, 1, 1, true> : k_firstq<8, 3, 1, 1, false>;
             return l->conj ? k_firstq<8, 3, 1, -1, true> : k_firstq<8, 3, 1, -1, false>;
         }

@@ -21,9 +21,9 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 # (kernel-name regex on the mangled name, max VGPR spill dwords)
 BUDGETS = [
-    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]ELb0E", 0),  # 2^20 pass A (c2)
+    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]EE", 0),  # 2^20 pass A (c2)
     (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]ELb0E", 0),  # 2^20 pass B (c2)
-    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]ELb0E", 0),  # 2^21 pass A (c5)
+    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]EE", 0),  # 2^21 pass A (c5)
     (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0),  # r2c split (c5)
     (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1E", 0),  # 12600 row (c3)
     (r"^_ZN3bxc6k_bxcdILin?1ELb0E", 8),  # persistent Bluestein (c4): 8 dwords, intrinsic
