@@ -99,6 +99,9 @@ int mr_has_variant(const hsd_pass *p);
  * h+1 bins (hsfft_r2c_batched_compact) instead of the mirrored N */
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
                  long long B, int batch, int sgn, int compact);
+/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h); 1 = not applicable */
+int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
+                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng);
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
 int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
                  int conj, int dir, int sgn2, int conj2); /* hsfft_pass_mr.h has a kernel for this pass */

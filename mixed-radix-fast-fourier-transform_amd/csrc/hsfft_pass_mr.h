@@ -513,9 +513,9 @@ __device__ __forceinline__ void glds16(const double2 *g, double2 *lds_base)
 /* points of the next row prefetched by k_row2<..., PRE>: 132 wave-instructions of 64 */
 constexpr int ROW_PRE_PTS = 8448;
 
-/* PF: the inputs of the next row's first 9-point group (55 % of a row at TPG = 768) are
- * loaded into registers right after this row's first exchange, so their latency overlaps
- * this row's remaining stages (needs the VGPRs of TPG = 768: 168 per thread) */
+/* PF: the inputs of the next row's first PF 9-point groups (37 % of a row per group at
+ * TPG = 512) are loaded into registers right after this row's first exchange, so their
+ * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
@@ -755,26 +755,21 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true, true>;
         /* default: 512 threads (8 waves, 256 VGPRs per thread) with the next row's first input
          * group (37 % of the row) loaded into registers during this row's stages 2-5: 113.5 ->
-         * 123.5 GSamples/s; HSFFT_ROW_T=1024 (16 waves, 128 VGPRs) / 768 (168 VGPRs) and
-         * HSFFT_ROW_PF=0/1/2 (groups prefetched) select the other variants */
+         * 123.5 GSamples/s; HSFFT_ROW_T=1024 (16 waves, 128 VGPRs: round 1's kernel) / 768 (168
+         * VGPRs) without prefetch, HSFFT_ROW_PF=0 the 512-thread kernel without it.  The
+         * prefetching 768 / 1024-thread kernels (25 / 21 dwords of spill) and the two-group
+         * prefetch (4 dwords, no faster) were measured and removed */
         const char *et = getenv("HSFFT_ROW_T"), *epf = getenv("HSFFT_ROW_PF");
-        const int rt = et ? atoi(et) : 512, rpf = epf ? atoi(epf) : (rt == 512 ? 1 : 0);
+        const int rt = et ? atoi(et) : 512, rpf = epf ? atoi(epf) : 1;
         int threads = 1024;
         if (f01 && !rpre && rt == 768) {
             threads = 768;
-            fn = rpf ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 768, true, true, false, 1>
-                               : k_row2<3, 3, 5, 5, 7, 8, 768, false, true, false, 1>)
-                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 768, true, true> : k_row2<3, 3, 5, 5, 7, 8, 768, false, true>);
-        } else if (f01 && !rpre && rt == 512) { /* 8 waves, 256 VGPRs: room for 2 of 3 groups */
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 768, true, true> : k_row2<3, 3, 5, 5, 7, 8, 768, false, true>;
+        } else if (f01 && !rpre && rt == 512) { /* 8 waves, 256 VGPRs: room for one group */
             threads = 512;
-            fn = rpf >= 2 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 2>
-                                    : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 2>)
-               : rpf == 1 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
-                                    : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>)
-                          : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true> : k_row2<3, 3, 5, 5, 7, 8, 512, false, true>);
-        } else if (f01 && !rpre && rpf) {
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true, false, 1>
-                        : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true, false, 1>;
+            fn = rpf ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
+                               : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>)
+                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true> : k_row2<3, 3, 5, 5, 7, 8, 512, false, true>);
         }
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));

@@ -490,9 +490,7 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"},
                                  {"HSFFT_ROW_T": "1024", "HSFFT_ROW_PRE": "1"}, {"HSFFT_ROW_T": "1024"},
-                                 {"HSFFT_ROW_T": "768"}, {"HSFFT_ROW_T": "768", "HSFFT_ROW_PF": "1"},
-                                 {"HSFFT_ROW_T": "1024", "HSFFT_ROW_PF": "1"}, {"HSFFT_ROW_T": "512", "HSFFT_ROW_PF": "0"},
-                                 {"HSFFT_ROW_T": "512", "HSFFT_ROW_PF": "2"}])
+                                 {"HSFFT_ROW_T": "768"}, {"HSFFT_ROW_T": "512", "HSFFT_ROW_PF": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -501,7 +499,7 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     exactly ONE row, so no row can lean on an earlier row's barriers (the stage-1 twiddles of
     the fused first stages are read right after the per-workgroup LDS copy).  Variants:
     mr::k_row2 (default: 512 threads, the next row's first input group prefetched into
-    registers) with 1024 / 768 threads, with 0 / 2 groups prefetched, stages 0-1 unfused,
+    registers) with 1024 / 768 threads, without the prefetch, stages 0-1 unfused,
     mr::k_row (one workgroup per row), the two mixed-radix passes, the LDS-DMA prefetch."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
