@@ -1,0 +1,90 @@
+// c1 latency floor probe (timing only, no FFT): what one small host-buffer call costs on
+// this box before any transform work.
+//   a) empty kernel + hipStreamSynchronize
+//   b) empty kernel whose last store sets a flag in page-locked host memory; the host polls
+//      the flag (no stream wait)
+//   c) kernel copying 16 KB from one page-locked host buffer to another (the zero-copy
+//      pattern of the small fft_exec path) + hipStreamSynchronize
+// Build: hipcc -O2 --offload-arch=gfx950 c1_latency.hip -o c1_latency (binary git-ignored)
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return 1;                                                                  \
+        }                                                                              \
+    } while (0)
+
+__global__ void k_empty() {}
+
+__global__ void k_flag(volatile unsigned *flag, unsigned v)
+{
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        *flag = v; /* vector store to host memory */
+    }
+}
+
+__global__ void k_copy(const double2 *in, double2 *out, int n)
+{
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = in[i];
+}
+
+static double med(std::vector<double> v)
+{
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+int main()
+{
+    using clk = std::chrono::steady_clock;
+    hipStream_t st;
+    CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    unsigned *flag;
+    CK(hipHostMalloc((void **)&flag, 64, hipHostMallocCoherent));
+    double2 *hin, *hout;
+    CK(hipHostMalloc((void **)&hin, 16384, hipHostMallocDefault));
+    CK(hipHostMalloc((void **)&hout, 16384, hipHostMallocDefault));
+    for (int i = 0; i < 1024; i++) hin[i] = make_double2(i, -i);
+    const int R = 2000;
+    std::vector<double> ta, tb, tc;
+    for (int r = 0; r < R + 100; r++) {
+        auto t0 = clk::now();
+        hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st);
+        CK(hipStreamSynchronize(st));
+        auto t1 = clk::now();
+        *(volatile unsigned *)flag = 0;
+        hipLaunchKernelGGL(k_flag, dim3(1), dim3(64), 0, st, (volatile unsigned *)flag, (unsigned)(r + 1));
+        long spins = 0;
+        while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != (unsigned)(r + 1))
+            if (++spins > 2000000000L) {
+                fprintf(stderr, "flag never arrived\n");
+                return 1;
+            }
+        auto t2 = clk::now();
+        CK(hipStreamSynchronize(st)); /* drain before the next timing (outside t) */
+        auto t3 = clk::now();
+        hipLaunchKernelGGL(k_copy, dim3(1), dim3(256), 0, st, (const double2 *)hin, hout, 1024);
+        CK(hipStreamSynchronize(st));
+        auto t4 = clk::now();
+        if (r >= 100) {
+            ta.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+            tb.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
+            tc.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
+        }
+    }
+    if (hout[1023].x != 1023.0) {
+        fprintf(stderr, "copy check failed\n");
+        return 1;
+    }
+    printf("median us: empty+sync %.2f | empty+host-flag poll %.2f | 16KB pinned->pinned copy kernel+sync %.2f\n",
+           med(ta), med(tb), med(tc));
+    return 0;
+}
