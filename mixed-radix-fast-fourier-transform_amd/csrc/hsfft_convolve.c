@@ -215,6 +215,10 @@ int hsfft_convolve_batched(const char *type, const char *conv_type, const fft_ty
     if (!d_a || !d_b || !d_out || length1 <= 0 || length2 <= 0 || batch < 0) return HSFFT_ERR_ARG;
     int linear, clen, P, start;
     if (conv_setup(conv_type, length1, length2, &linear, &clen, &P)) return HSFFT_ERR_ARG;
+    if (P < 2) { /* both lengths 1: the reference's real plan of length 1 exits (real.c:26-31) */
+        hs_seterr("convolution of two length-1 signals: transform length %d is not even", P);
+        return HSFFT_ERR_ARG;
+    }
     const int len = conv_window(type, linear, clen, P, length1, length2, &start);
     if (len < 0) return HSFFT_ERR_ARG;
     if (batch == 0) return len;

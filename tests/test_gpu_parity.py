@@ -268,6 +268,37 @@ def test_c2r_batched_matches_oracle(n, rows):
         assert np.max(np.abs(y / n - x)) < 1e-12
 
 
+def test_real_every_even_length_2_to_4096():
+    """r2c (both plan signs) and c2r of every even length 2..4096, 2 device-resident rows,
+    bit-exact vs the oracle (ref real.c:80-193: the N/2-point inner c2c of every
+    factorisation, then the split / pre-twiddle)."""
+    bad = []
+    for n in range(2, 4097, 2):
+        x = T.real_input(n, 0x7A7A ^ n, batch=2).reshape(2, n)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(2 * n * 16)
+        for sgn in (1, -1):
+            rp = hsfft.RealPlan(n, sgn)
+            hsfft.r2c_batched(rp, din, dout, 2)
+            y = dout.to_array(np.complex128).reshape(2, n)
+            if not T.bits_equal(y, T.oracle_r2c(x, sgn)):
+                bad.append(("r2c", n, sgn))
+            rp.close()
+        X = T.oracle_r2c(x, 1)
+        dX = hsfft.DeviceBuffer.from_array(X)
+        dy = hsfft.DeviceBuffer(2 * n * 8)
+        rp = hsfft.RealPlan(n, -1)
+        hsfft.c2r_batched(rp, dX, dy, 2)
+        y = dy.to_array(np.float64).reshape(2, n)
+        for b in range(2):
+            if not T.bits_equal(y[b], T.oracle_c2r(X[b], n, -1)):
+                bad.append(("c2r", n, b))
+        rp.close()
+        for buf in (din, dout, dX, dy):
+            buf.free()
+    assert not bad, bad[:20]
+
+
 def test_convolve_fixtures(golden):
     meta, data = golden
     L = hsfft.lib()
@@ -300,6 +331,42 @@ def test_convolve_batched_matches_oracle():
             assert lib.orc_convolve(typ, b"linear", T.ptr(np.ascontiguousarray(a[r])), n,
                                     T.ptr(np.ascontiguousarray(b[r])), m, T.ptr(o), 0) == ln
             assert T.bits_equal(y[r], o[:ln]), (typ, r)
+
+
+def test_convolve_batched_sweep():
+    """hsfft_convolve_batched over 47 signal lengths x 6 kernel lengths (either one the longer,
+    P = 2 .. 2048), linear full / same / valid and circular, 2 rows each: bit-exact vs the
+    oracle's convolve.c:20-214 (P = next power of two of the output length)."""
+    L, lib = hsfft.lib(), T.oracle()
+    rows, bad, calls = 2, [], 0
+    for n in range(1, 600, 13):
+        for m in (1, 2, 5, 64, 200, 511):
+            a = T.real_input(n, 0x11 ^ n, batch=rows).reshape(rows, n)
+            b = T.real_input(m, 0x22 ^ m, batch=rows).reshape(rows, m)
+            da, db = hsfft.DeviceBuffer.from_array(a), hsfft.DeviceBuffer.from_array(b)
+            dout = hsfft.DeviceBuffer(rows * 2 * (n + m) * 8)
+            for typ, ct in ((b"full", b"linear"), (b"same", b"linear"), (b"valid", b"linear"),
+                            (b"full", b"circular")):
+                ln = L.hsfft_convolve_batched(typ, ct, da.ptr, n, db.ptr, m, dout.ptr, rows)
+                calls += 1
+                if n == m == 1:  # P = 1: the reference's length-1 real plan exits; an error here
+                    if ln >= 0:
+                        bad.append((n, m, typ, ct, "P=1 accepted"))
+                    continue
+                if ln <= 0:
+                    bad.append((n, m, typ, ct, "rc", ln))
+                    continue
+                y = dout.to_array(np.float64, rows * ln).reshape(rows, ln)
+                for r in range(rows):
+                    o = np.zeros(4 * (n + m))
+                    want = lib.orc_convolve(typ, ct, T.ptr(np.ascontiguousarray(a[r])), n,
+                                            T.ptr(np.ascontiguousarray(b[r])), m, T.ptr(o), 0)
+                    if want != ln or not T.bits_equal(y[r], o[:ln]):
+                        bad.append((n, m, typ, ct, r))
+            for buf in (da, db, dout):
+                buf.free()
+    assert calls == 47 * 6 * 4
+    assert not bad, bad[:20]
 
 
 @pytest.mark.parametrize("n,m,typ", [(1 << 16, 1000, b"full"), (70000, 70000, b"same"), (5000, 300, b"valid")])

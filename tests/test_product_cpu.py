@@ -180,3 +180,18 @@ def test_compute_fails_loudly_without_gpu():
     assert r.returncode == 1
     assert "UNREACHABLE" not in r.stdout
     assert "no HIP device" in r.stderr or "MI355X" in r.stderr
+
+
+def test_convolve_batched_argument_errors():
+    """hsfft_convolve_batched validates before touching a device: bad types and two length-1
+    signals (transform length 1, which the reference's real plan rejects by exiting,
+    real.c:26-31) return HSFFT_ERR_ARG (-1) instead; batch 0 returns the output length."""
+    L = hsfft.lib()
+    buf = ctypes.c_void_p(16)  # never dereferenced on these paths
+    assert L.hsfft_convolve_batched(b"full", b"linear", buf, 1, buf, 1, buf, 2) == -1
+    assert L.hsfft_convolve_batched(b"full", b"circular", buf, 1, buf, 1, buf, 2) == -1
+    assert L.hsfft_convolve_batched(b"full", b"spiral", buf, 8, buf, 3, buf, 2) == -1
+    assert L.hsfft_convolve_batched(b"middle", b"linear", buf, 8, buf, 3, buf, 2) == -1
+    assert L.hsfft_convolve_batched(b"full", b"linear", buf, 8, buf, 3, buf, 0) == 10
+    assert L.hsfft_convolve_batched(b"valid", b"linear", buf, 8, buf, 3, buf, 0) == 6
+    assert L.hsfft_convolve_batched(b"full", b"circular", buf, 5, buf, 3, buf, 0) == 8
