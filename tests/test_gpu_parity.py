@@ -269,9 +269,10 @@ def test_c2r_batched_matches_oracle(n, rows):
 
 
 def test_real_every_even_length_2_to_4096():
-    """r2c (both plan signs) and c2r of every even length 2..4096, 2 device-resident rows,
-    bit-exact vs the oracle (ref real.c:80-193: the N/2-point inner c2c of every
-    factorisation, then the split / pre-twiddle)."""
+    """r2c (both plan signs, reference layout and the compact N/2+1-bin extension) and c2r of
+    every even length 2..4096, 2 device-resident rows, bit-exact vs the oracle (ref
+    real.c:80-193: the N/2-point inner c2c of every factorisation, then the split or the
+    pre-twiddle)."""
     bad = []
     for n in range(2, 4097, 2):
         x = T.real_input(n, 0x7A7A ^ n, batch=2).reshape(2, n)
@@ -281,8 +282,14 @@ def test_real_every_even_length_2_to_4096():
             rp = hsfft.RealPlan(n, sgn)
             hsfft.r2c_batched(rp, din, dout, 2)
             y = dout.to_array(np.complex128).reshape(2, n)
-            if not T.bits_equal(y, T.oracle_r2c(x, sgn)):
+            want = T.oracle_r2c(x, sgn)
+            if not T.bits_equal(y, want):
                 bad.append(("r2c", n, sgn))
+            h1 = n // 2 + 1  # compact extension: the first N/2+1 bins of the same rows
+            hsfft.r2c_batched_compact(rp, din, dout, 2)
+            yc = dout.to_array(np.complex128, 2 * h1).reshape(2, h1)
+            if not T.bits_equal(yc, np.ascontiguousarray(want[:, :h1])):
+                bad.append(("r2c compact", n, sgn))
             rp.close()
         X = T.oracle_r2c(x, 1)
         dX = hsfft.DeviceBuffer.from_array(X)
