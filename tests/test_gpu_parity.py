@@ -136,6 +136,22 @@ def test_c2c_every_length_2_to_8192():
     assert not bad, bad[:20]
 
 
+def test_c2c_dropin_every_length_2_to_4096():
+    """the drop-in fft_exec on host buffers (one-pass plans take the page-locked zero-copy
+    path, the others the staged path) for every length 2..4096, alternating signs, bit-exact
+    vs the oracle (highSpeedFFT.c:1920-1942 fft_exec)."""
+    bad = []
+    for n in range(2, 4097):
+        sgn = 1 if n % 2 else -1
+        x = T.complex_input(n, T.seed_for(n) ^ 0x6161)
+        p = hsfft.Plan(n, sgn)
+        y = p.exec(x)
+        p.close()
+        if not T.bits_equal(y, oracle_rows(x, sgn)):
+            bad.append((n, sgn))
+    assert not bad, bad[:20]
+
+
 def test_c2c_matches_reference_fixtures(golden):
     """Golden outputs of the reference itself.  'asis' cases whose factor list ends in 2 are
     D1-affected (their output depends on the caller's buffer) and are covered by the 'fixed'
