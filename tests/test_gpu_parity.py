@@ -136,6 +136,24 @@ def test_c2c_every_length_2_to_8192():
     assert not bad, bad[:20]
 
 
+def test_c2c_exact_twiddle_mode_every_length_2_to_8192():
+    """the reference's USE_TWIDDLE_TABLES-off build (every stage twiddle from sincos;
+    hsfft_set_twiddle_mode("exact")) for every length 2..8192, alternating signs, 2 rows,
+    bit-exact vs the oracle with ORC_TWIDDLE_EXACT."""
+    bad = []
+    hsfft.set_twiddle_mode("exact")
+    try:
+        for n in range(2, 8193):
+            sgn = 1 if n % 2 else -1
+            x = T.complex_input(n, T.seed_for(n) ^ 0x4E4E, batch=2).reshape(2, n)
+            y = gpu_c2c_batched(n, sgn, x)
+            if not T.bits_equal(y, oracle_rows(x, sgn, flags=1)):
+                bad.append((n, sgn))
+    finally:
+        hsfft.set_twiddle_mode("reference")
+    assert not bad, bad[:20]
+
+
 def test_c2c_dropin_every_length_2_to_4096():
     """the drop-in fft_exec on host buffers (one-pass plans take the page-locked zero-copy
     path, the others the staged path) for every length 2..4096, alternating signs, bit-exact
