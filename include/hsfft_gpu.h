@@ -98,6 +98,12 @@ int hsfft_time_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *
  * d_dst, event-timed; the practical HBM ceiling reported next to the FFT numbers. */
 int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms);
 
+/* Bluestein M = 2^18 (e.g. N = 99991) runs as one persistent launch whose workgroups must all
+ * be resident; when something else holds CUs its in-launch waits time out and the rows are
+ * re-run on the three-launch path (same results, more time).  Count of such re-runs in this
+ * process. */
+long long hsfft_bluestein_fallbacks(void);
+
 /* --- threading -------------------------------------------------------------------------
  * Every entry point is safe to call from several host threads at once, on shared or
  * distinct plans (the reference's mixed-radix fft_exec is reentrant, highSpeedFFT.c:1920).

@@ -217,9 +217,8 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
 
 /* Inverse FFT's second pass [8,8,8] at L = B = 512 (sign -S, conjugated twiddles) of q-tile
  * q0 for T rows, stored through the chirp for n < nsig (direction S).  Row prefetch (PREF)
- * is opt-in (HSFFT_BLUE_PREF=1), as for pf::k_b512: with it the kernel spills 20 B. */
-/* PROBE (timing only, HSFFT_BLUE_PROBE=1; results WRONG): no chirp loads in the store loop */
-template <int T, int S, bool PREF = true, bool SPLIT = false, bool PROBE = false>
+ * is a template option the launcher does not use (as for pf::k_b512: with it the kernel spills 20 B). */
+template <int T, int S, bool PREF = true, bool SPLIT = false>
 __global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -309,7 +308,7 @@ __global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
             const unsigned n = (jt + jj * TPG) * B + q;
-            if (n < nsig) orow[n] = chirp_out<S>(xr[jj], xi[jj], PROBE ? make_double2(1.0, 0.0) : ch[n]);
+            if (n < nsig) orow[n] = chirp_out<S>(xr[jj], xi[jj], ch[n]);
         }
     }
 }
@@ -328,28 +327,14 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
 {
     const int mask = env("HSFFT_BLUE_PF", 7);
     if (!((mask >> which) & 1) || (sgn != 1 && sgn != -1)) return 1;
-    const int t = env("HSFFT_BLUE_T", 8); /* measured c4: T 2 17.8, 4 18.7, 8 19.1 GS/s */
-    const int T = t >= 8 ? 8 : t >= 4 ? 4 : t >= 2 ? 2 : 1;
+    /* 8 rows per workgroup (measured c4: T 2 17.8, 4 18.7, 8 19.1 GS/s); the last kernel without
+     * a row prefetch (20.98 vs 20.26 GS/s with it: it spills); the split-exchange variants
+     * (three workgroups per CU) measured +0.6 % / -5 % and were removed in round 3 */
+    constexpr int T = 8;
     kfn fn;
-    /* HSFFT_BLUE_SPLIT bit 0: k_bfirst, bit 1: k_blast with the split exchange (3 per CU) */
-    const int split = env("HSFFT_BLUE_SPLIT", 0);
-    const bool sp = (which == 2 && (split & 1)) || (which == 1 && (split & 2));
-    if (which == 2 && sp && T == 8)
-        fn = sgn == 1 ? k_bfirst<8, 1, true> : k_bfirst<8, -1, true>;
-    else if (which == 1 && sp && T == 8)
-        fn = sgn == 1 ? k_blast<8, 1, false, true> : k_blast<8, -1, false, true>;
-    else if (which == 2)
-        fn = sgn == 1 ? (T == 8 ? k_bfirst<8, 1> : T == 4 ? k_bfirst<4, 1> : T == 2 ? k_bfirst<2, 1> : k_bfirst<1, 1>)
-                      : (T == 8 ? k_bfirst<8, -1> : T == 4 ? k_bfirst<4, -1> : T == 2 ? k_bfirst<2, -1> : k_bfirst<1, -1>);
-    else if (which == 0)
-        fn = sgn == 1 ? (T == 8 ? k_bmid<8, 1> : T == 4 ? k_bmid<4, 1> : T == 2 ? k_bmid<2, 1> : k_bmid<1, 1>)
-                      : (T == 8 ? k_bmid<8, -1> : T == 4 ? k_bmid<4, -1> : T == 2 ? k_bmid<2, -1> : k_bmid<1, -1>);
-    else if (T == 8 && !env("HSFFT_BLUE_PREF", 0)) /* c4: 20.98 vs 20.26 GS/s with the prefetch (spills) */
-        fn = env("HSFFT_BLUE_PROBE", 0) ? (sgn == 1 ? k_blast<8, 1, false, false, true> : k_blast<8, -1, false, false, true>)
-                                        : (sgn == 1 ? k_blast<8, 1, false> : k_blast<8, -1, false>);
-    else
-        fn = sgn == 1 ? (T == 8 ? k_blast<8, 1> : T == 4 ? k_blast<4, 1> : T == 2 ? k_blast<2, 1> : k_blast<1, 1>)
-                      : (T == 8 ? k_blast<8, -1> : T == 4 ? k_blast<4, -1> : T == 2 ? k_blast<2, -1> : k_blast<1, -1>);
+    if (which == 2) fn = sgn == 1 ? k_bfirst<8, 1> : k_bfirst<8, -1>;
+    else if (which == 0) fn = sgn == 1 ? k_bmid<8, 1> : k_bmid<8, -1>;
+    else fn = sgn == 1 ? k_blast<8, 1, false> : k_blast<8, -1, false>;
     Args a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)in;
@@ -371,7 +356,7 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     const long long grid = a.tiles * ((batch + T - 1) / T);
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     /* image + twiddle runs (k_bfirst: 511; k_bmid: 504 forward runs + 511 inverse entries) */
-    const size_t lds = (size_t)((sp && T == 8 ? 512 * 4 : 512 * 8) + (which == 0 ? 1016 : 512)) * sizeof(double2);
+    const size_t lds = (size_t)(512 * 8 + (which == 0 ? 1016 : 512)) * sizeof(double2);
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a);
     HCHK(hipGetLastError());

@@ -27,11 +27,24 @@
  * pass) and the tile's forward runs (P2; conjugated for P3) in LDS, the tile's stage-2
  * twiddles in registers.
  *
- * Hand-off (MI355X_MICROARCH.md visibility table, row 1): images are
- * written with sc1 stores, every wave waits vmcnt(0), a workgroup barrier, one lane adds 1
- * (relaxed, agent scope) to the group's counter; waiters poll it (relaxed agent loads, bounded
- * by a ~10 s real-time deadline that sets the sticky error word), join a barrier and read the
- * image with sc1 loads.
+ * Hand-off (cdna_hip_programming.md Guideline 16, recipe R1 -- valid at any number of
+ * workgroups per CU): images are written with 16-B sc1 (write-through) stores, every wave
+ * waits vmcnt(0), a workgroup barrier, then ONE lane adds 1 (relaxed, agent scope) to the
+ * group's counter.  The consumer's lane 0 polls that counter (relaxed agent loads, bounded by
+ * a ~1.3 s real-time deadline that sets the sticky error word), then ONE agent-scope acquire
+ * (buffer_inv sc1) + vmcnt(0), then the workgroup barrier, then the image loads (sc1 loads,
+ * L2-served).  Round 2 ran without the acquire, relying on sc1 loads alone; that form is
+ * validated only for one workgroup per CU (MI355X_MICROARCH.md, Valid forms, row 1), and this
+ * launch runs two, so the acquire is back.
+ *
+ * Residency: every workgroup of a group waits on the others, so the whole grid must be
+ * resident.  The host checks the occupancy API; if something else occupies the GPU the waits
+ * time out, the kernel exits, and the host re-runs the rows through the three-launch path
+ * (hsfft_exec.c run_bluestein), so a busy GPU costs time, never results.
+ *
+ * Uneven-load testing: a.jitter > 0 adds a pseudo-random s_sleep (0 .. jitter-1 units of
+ * ~4 us) to each workgroup before its arrive and after its wait, per phase -- results are
+ * unchanged, the order in which workgroups hand over is scrambled.
  *
  * Arithmetic: the exact operation sequence of k_bfirst / k_bmid / k_blast (pf::stage,
  * r8::exchange, spec, chirp_out) -- bit-identical to them and to the CPU reference
@@ -41,7 +54,7 @@
 
 namespace bxc {
 
-constexpr unsigned long long T_LIMIT = 1ull << 30; /* bounded waits: ~10 s of the 100 MHz real-time counter */
+constexpr unsigned long long T_LIMIT = 1ull << 27; /* bounded waits: ~1.3 s of the 100 MHz real-time counter */
 
 constexpr unsigned NTILE = 64;  /* 8-column tiles of the 512 x 512 image = workgroups per group */
 constexpr unsigned CS = 32;     /* counter stride (128-B line per counter) */
@@ -60,47 +73,63 @@ struct XArgs {
     unsigned *cnt;        /* [ng][2] counters, CS apart */
     unsigned *err;        /* sticky error word */
     unsigned batch, ng, nsig, sleep;
+    unsigned jitter;      /* > 0: pseudo-random per-phase delays (uneven-load tests; results unchanged) */
     unsigned xmap;        /* 1: a group spans the XCDs (XCD x owns tiles [8x, 8x+8) of every group) */
     unsigned *dbg;        /* optional per-workgroup trace (8 words): rows, P1, wait A, P2, wait B, P3 */
 };
 
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
-template <bool SC1 = true>
 __device__ __forceinline__ void st_sc1(const __amdgpu_buffer_rsrc_t &rs, unsigned voff, unsigned soff, double x, double y)
 {
     const double2 v = make_double2(x, y);
     u4 u;
     __builtin_memcpy(&u, &v, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(u, rs, voff, soff, SC1 ? 16 : 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u, rs, voff, soff, 16); /* aux 16 = sc1: write-through */
 }
 
-template <bool SC1 = true>
 __device__ __forceinline__ double2 ld_sc1(const __amdgpu_buffer_rsrc_t &rs, unsigned voff, unsigned soff)
 {
-    const u4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, SC1 ? 16 : 0);
+    const u4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 16);
     double2 d;
     __builtin_memcpy(&d, &u, 16);
     return d;
 }
 
-/* this workgroup's image stores are done: count it in */
-__device__ __forceinline__ void arrive(unsigned *c)
+/* uneven-load test delay: 0 .. jitter-1 units of s_sleep 64 (~4 us at 1 GHz..2.4 GHz clocks
+ * it is 2.7-6.5 us), chosen per (workgroup, phase, row) by a hash; thread 0 sleeps, the
+ * barrier that follows holds the rest of the workgroup */
+__device__ __forceinline__ void jitter_sleep(const XArgs &a, unsigned k, unsigned ph)
+{
+    if (a.jitter == 0 || threadIdx.x != 0) return;
+    unsigned h = (blockIdx.x * 0x9E3779B1u) ^ (k * 0x85EBCA77u) ^ (ph * 0xC2B2AE3Du);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    for (unsigned n = h % a.jitter; n; n--) __builtin_amdgcn_s_sleep(64);
+}
+
+/* this workgroup's image stores are done: count it in (R1 producer: every storing wave drains
+ * its sc1 stores, the barrier, then one lane adds) */
+__device__ __forceinline__ void arrive(const XArgs &a, unsigned *c, unsigned k, unsigned ph)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    jitter_sleep(a, k, ph);
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* wait until the group's counter reaches `target`; false on timeout (~10 s without progress
- * of this one wait) / sticky error */
-__device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned target, unsigned *sflag)
+/* wait until the group's counter reaches `target` (R1 consumer: one lane polls relaxed, then
+ * ONE agent-scope acquire and its vmcnt(0), then the barrier every wave joins before loading);
+ * false on timeout (~1.3 s without progress of this one wait) or sticky error */
+__device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned target, unsigned *sflag, unsigned k,
+                                      unsigned ph)
 {
     if (threadIdx.x == 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); /* deadline per wait */
         unsigned bad = 0;
         while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            for (unsigned k = 0; k < a.sleep; k++) __builtin_amdgcn_s_sleep(2);
+            for (unsigned n = 0; n < a.sleep; n++) __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > T_LIMIT ||
                 __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -108,16 +137,16 @@ __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned targ
                 break;
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); /* buffer_inv sc1: drop this CU's stale L1 lines */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the invalidate has completed */
         *sflag = bad;
     }
+    jitter_sleep(a, k, ph + 8);
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keep the image loads below the poll */
     return __builtin_amdgcn_readfirstlane(*sflag) == 0;
 }
 
-/* PLAIN (timing probe only, HSFFT_BX_PLAIN=1): image stores / loads without sc1 -- NOT a
- * valid hand-off unless every workgroup of a group shares one L2 */
-template <int S, bool PLAIN = false>
+template <int S>
 __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -185,7 +214,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
         double xr[8], xi[8];
         double2 w[7];
         if (k >= 2) { /* ---- P3 of row k-2: k_blast's body on image 2 [k&1], chirp store */
-            if (!await(a, cB, (k - 1) * NTILE, sflag)) return;
+            if (!await(a, cB, (k - 1) * NTILE, sflag, k, 0)) return;
             BX_MARK(4)
             /* per-thread indices from an opaque copy of threadIdx in every phase, so the
              * compiler does not hoist all three phases' addresses out of the loop (spills) */
@@ -197,7 +226,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
                 __builtin_amdgcn_make_buffer_rsrc(imgs + (2 + (k & 1)) * (size_t)IMG, 0, (int)(IMG * 16u), 0x00020000);
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const double2 v = ld_sc1<!PLAIN>(r2, col, i * TPG * B * 16);
+                const double2 v = ld_sc1(r2, col, i * TPG * B * 16);
                 xr[i] = v.x;
                 xi[i] = v.y;
             }
@@ -228,7 +257,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
             tr[0]++;
         }
         if (k >= 1 && k <= R) { /* ---- P2 of row k-1: k_bmid's body, image 1 -> image 2 [(k-1)&1] */
-            if (!await(a, cA, k * NTILE, sflag)) return;
+            if (!await(a, cA, k * NTILE, sflag, k, 1)) return;
             BX_MARK(2)
             unsigned tt = tid;
             asm volatile("" : "+v"(tt));
@@ -241,7 +270,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
                 __builtin_amdgcn_make_buffer_rsrc(imgs + (2 + par) * (size_t)IMG, 0, (int)(IMG * 16u), 0x00020000);
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const double2 v = ld_sc1<!PLAIN>(r1, col, i * TPG * B * 16);
+                const double2 v = ld_sc1(r1, col, i * TPG * B * 16);
                 xr[i] = v.x;
                 xi[i] = v.y;
             }
@@ -267,9 +296,9 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
             pf::tw8_lds<true>(w, t0, 64, jt & 63);
             pf::stage<8, -S>(xr, xi, w, false);
 #pragma unroll
-            for (int jj = 0; jj < 8; jj++) st_sc1<!PLAIN>(r2, rowo, jj * TPG * 16, xr[jj], xi[jj]);
+            for (int jj = 0; jj < 8; jj++) st_sc1(r2, rowo, jj * TPG * 16, xr[jj], xi[jj]);
             BX_MARK(3)
-            arrive(cB);
+            arrive(a, cB, k, 2);
             BX_MARK(7)
         }
         if (k < R) { /* ---- P1 of row k: k_bfirst's body (columns m = q) -> image 1 [k&1] */
@@ -311,9 +340,9 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
             for (int i = 0; i < 7; i++) w[i] = t0[63 + 7 * (jt & 63) + i];
             pf::stage<8, S>(xr, xi, w, false);
 #pragma unroll
-            for (int jj = 0; jj < 8; jj++) st_sc1<!PLAIN>(r1, rowo, jj * TPG * 16, xr[jj], xi[jj]);
+            for (int jj = 0; jj < 8; jj++) st_sc1(r1, rowo, jj * TPG * 16, xr[jj], xi[jj]);
             BX_MARK(1)
-            arrive(cA);
+            arrive(a, cA, k, 3);
             BX_MARK(6)
         }
     }

@@ -547,9 +547,7 @@ int grid_for(long long n, int threads)
 
 #include "hsfft_pass_r8.h"
 #include "hsfft_pass_pf.h"
-#include "hsfft_pass_wl.h"
 #include "hsfft_pass_mr.h"
-#include "hsfft_fused.h"
 #include "hsfft_blue_pf.h"
 #include "hsfft_blue_xcd.h"
 
@@ -619,27 +617,27 @@ int hsd_memset_async(void *d, int v, size_t bytes)
     return 0;
 }
 
-/* fused-launch state per device: counter block (heads, error word, per-group counters) and
- * a pinned host copy of the sticky error word, checked at every synchronisation */
-static unsigned *g_fz_ctr[HS_MAX_DEV];
-static size_t g_fz_bytes[HS_MAX_DEV];
-static unsigned *g_fz_err_host[HS_MAX_DEV];
+/* persistent-launch state per device (bxc::k_bxcd): a counter block (per-group counters, the
+ * sticky error word) and a pinned host copy of the error word */
+static unsigned *g_pl_ctr[HS_MAX_DEV];
+static size_t g_pl_bytes[HS_MAX_DEV];
+static unsigned *g_pl_err_host[HS_MAX_DEV];
 
-static int fz_check(void)
+/* the sticky error word of the last persistent launch (set when a wait timed out) */
+static int pl_check(void)
 {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV || !g_fz_err_host[dev]) return 0;
-    if (*(volatile unsigned *)g_fz_err_host[dev] == 0) return 0;
-    *g_fz_err_host[dev] = 0;
-    HCHK(hipMemset(g_fz_ctr[dev] + fz::NQ, 0, sizeof(unsigned)));
-    snprintf(g_err, sizeof g_err, "fused launch: an in-launch dependency wait timed out (results invalid)");
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV || !g_pl_err_host[dev]) return 0;
+    if (*(volatile unsigned *)g_pl_err_host[dev] == 0) return 0;
+    *g_pl_err_host[dev] = 0;
+    snprintf(g_err, sizeof g_err, "persistent launch: an in-launch dependency wait timed out (results invalid)");
     return -2;
 }
 
 int hsd_sync(void)
 {
     HCHK(hipStreamSynchronize(primary()));
-    return fz_check();
+    return pl_check();
 }
 
 /* wait for the library stream by polling an event (no blocking wait / wake-up): for short
@@ -659,117 +657,15 @@ int hsd_sync_spin(void)
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) return set_err(e, "hipEventQuery");
     }
-    return fz_check();
-}
-
-int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
-                int conj, int rows_per_group, int lag, int grid)
-{
-    int dev = 0;
-    HCHK(hipGetDevice(&dev));
-    if (dev < 0 || dev >= HS_MAX_DEV) return -1;
-    const int R = rows_per_group;
-    if ((R != 1 && R != 2 && R != 4) || batch < R || batch % R || (sgn != 1 && sgn != -1) || grid < fz::NQ ||
-        grid % fz::NQ) {
-        snprintf(g_err, sizeof g_err, "hsd_fused20: unsupported geometry (R=%d batch=%d grid=%d)", R, batch, grid);
-        return -1;
-    }
-    const unsigned ng = (unsigned)(batch / R);
-    /* [0, 8): ticket heads, [8]: sticky error word, [12, 12 + ng): group counters; the
-     * per-call memset covers heads + counters only (16-B aligned blocks) */
-    const size_t need = (12 + (size_t)ng) * sizeof(unsigned);
-    if (g_fz_bytes[dev] < need) {
-        if (g_fz_ctr[dev]) {
-            HCHK(hipStreamSynchronize(stream()));
-            HCHK(hipFree(g_fz_ctr[dev]));
-        }
-        const size_t alloc = (need + 4095) & ~(size_t)4095;
-        HCHK(hipMalloc((void **)&g_fz_ctr[dev], alloc));
-        HCHK(hipMemset(g_fz_ctr[dev], 0, alloc));
-        g_fz_bytes[dev] = alloc;
-        if (!g_fz_err_host[dev]) {
-            HCHK(hipHostMalloc((void **)&g_fz_err_host[dev], 64, hipHostMallocDefault));
-            *g_fz_err_host[dev] = 0;
-        }
-    }
-    unsigned *ctr = g_fz_ctr[dev];
-    HCHK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned), stream()));
-    HCHK(hipMemsetAsync(ctr + 12, 0, ((size_t)ng * sizeof(unsigned) + 15) & ~(size_t)15, stream()));
-    fz::FArgs a;
-    a.in = (const double2 *)in;
-    a.out = (double2 *)out;
-    a.tw = (const double2 *)tw;
-    a.idist = idist;
-    a.odist = odist;
-    a.head = ctr;
-    a.err = ctr + 8;
-    a.done = ctr + 12;
-    a.ngroups = ng;
-    a.lag = (unsigned)(lag < 1 ? 1 : lag);
-    {
-        const char *e = getenv("HSFFT_FZ_SPIN");
-        a.spin_max = e ? (unsigned)atoi(e) : (4u << 20);
-    }
-    a.dbg = nullptr;
-    const char *dbgenv = getenv("HSFFT_FZ_DEBUG");
-    static unsigned *s_dbg = nullptr;
-    if (dbgenv && atoi(dbgenv)) {
-        if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, 8192 * 16 * sizeof(unsigned)));
-        if (grid > 8192) return -1;
-        HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 16 * sizeof(unsigned), stream()));
-        a.dbg = s_dbg;
-    }
-    const char *qe = getenv("HSFFT_FZ_Q"); /* pass-A items with 64-B paired loads (default) */
-    const bool qa = !(qe && atoi(qe) == 0);
-    fz::ffn fn = R == 1 ? fz::fused_fn<1>(sgn, conj, qa) : R == 2 ? fz::fused_fn<2>(sgn, conj, qa)
-                                                                 : fz::fused_fn<4>(sgn, conj, qa);
-    HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fz::LDS_BYTES));
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), fz::LDS_BYTES, stream(), a);
-    HCHK(hipGetLastError());
-    HCHK(hipMemcpyAsync(g_fz_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
-    if (a.dbg) { /* trace: per queue, tickets / A items / B items / spins summed over its workers */
-        static unsigned h[8192 * 16];
-        unsigned hc[16];
-        HCHK(hipStreamSynchronize(stream()));
-        HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 16 * sizeof(unsigned), hipMemcpyDeviceToHost));
-        HCHK(hipMemcpy(hc, ctr, sizeof hc, hipMemcpyDeviceToHost));
-        fprintf(stderr, "fz debug: R=%d ng=%u grid=%d heads", R, ng, grid);
-        for (int q = 0; q < 8; q++) fprintf(stderr, " %u", hc[q]);
-        fprintf(stderr, " err=%u done[0..3]=%u %u %u %u\n", hc[8], hc[12], ng > 1 ? hc[13] : 0, ng > 2 ? hc[14] : 0,
-                ng > 3 ? hc[15] : 0);
-        for (int q = 0; q < 8; q++) {
-            unsigned long long tk = 0, na = 0, nb = 0, sp = 0, ta = 0, tb = 0, tw = 0, pl = 0, pc = 0, ps = 0, pt = 0;
-            int workers = 0, idle = 0;
-            for (int b = q; b < grid; b += 8) {
-                tk += h[b * 16];
-                na += h[b * 16 + 2];
-                nb += h[b * 16 + 3];
-                sp += h[b * 16 + 4];
-                ta += h[b * 16 + 5];
-                tb += h[b * 16 + 6];
-                tw += h[b * 16 + 7];
-                pl += h[b * 16 + 8];
-                pc += h[b * 16 + 9];
-                ps += h[b * 16 + 10];
-                pt += h[b * 16 + 11];
-                workers++;
-                idle += h[b * 16] == 0;
-            }
-            fprintf(stderr,
-                    "  queue %d: workers %d (idle %d) tickets %llu A %llu B %llu spins %llu | us per A item %.2f, "
-                    "per B item %.2f, wait per B %.2f\n",
-                    q, workers, idle, tk, na, nb, sp, na ? ta / 100.0 / na : 0.0, nb ? tb / 100.0 / nb : 0.0,
-                    nb ? tw / 100.0 / nb : 0.0);
-            fprintf(stderr, "           A phases (us): load %.2f compute %.2f store-drain %.2f | ticket %.2f per item\n",
-                    na ? pl / 100.0 / na : 0.0, na ? pc / 100.0 / na : 0.0, na ? ps / 100.0 / na : 0.0,
-                    tk ? pt / 100.0 / tk : 0.0);
-        }
-    }
-    return 0;
+    return pl_check();
 }
 
 /* Bluestein M = 2^18 as one persistent launch (hsfft_blue_xcd.h).  img: ng x 4 x M points of
- * scratch.  Returns 1 if not applicable (geometry, or the grid would not be co-resident). */
+ * scratch.  Synchronous: the launch is followed by a stream synchronisation and a check of its
+ * error word.  Returns 0 on success, 1 if not applicable (geometry, or the grid would not be
+ * co-resident), 2 if an in-launch wait timed out (the workgroups were not all resident, e.g.
+ * another kernel held CUs: the caller re-runs the rows on the three-launch path), < 0 on a
+ * HIP error. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
                  const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng)
 {
@@ -779,9 +675,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     if (batch < 1 || (sgn != 1 && sgn != -1) || ng < 1 || ng > 64 || nsig < 1 || nsig > (long long)bxc::IMG ||
         img_bytes < (size_t)ng * bxc::NIMG * bxc::IMG * sizeof(double2))
         return 1;
-    const char *pe = getenv("HSFFT_BX_PLAIN");
-    void (*fn)(bxc::XArgs) = (pe && atoi(pe)) ? (sgn == 1 ? bxc::k_bxcd<1, true> : bxc::k_bxcd<-1, true>)
-                                              : (sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>);
+    void (*fn)(bxc::XArgs) = sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>;
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bxc::LDS_BYTES));
     const int grid = ng * (int)bxc::NTILE;
     {
@@ -791,24 +685,28 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         HCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         if ((long long)per_cu * cus < grid) return 1;
     }
+    /* counter block: [0, 32) the sticky error word (word 8) on its own line, then 2 counters
+     * per group, each on a 128-B line; zeroed as a whole (from the allocation's start, a
+     * multiple of 16 B: Guideline 16, re-initialise every call) before every launch */
     const size_t CS = bxc::CS;
     const size_t need = (CS + 2 * CS * (size_t)ng) * sizeof(unsigned);
-    if (g_fz_bytes[dev] < need) {
-        if (g_fz_ctr[dev]) {
+    if (g_pl_bytes[dev] < need) {
+        if (g_pl_ctr[dev]) {
             HCHK(hipStreamSynchronize(stream()));
-            HCHK(hipFree(g_fz_ctr[dev]));
+            HCHK(hipFree(g_pl_ctr[dev]));
+            g_pl_ctr[dev] = nullptr;
+            g_pl_bytes[dev] = 0;
         }
         const size_t alloc = (need + 4095) & ~(size_t)4095;
-        HCHK(hipMalloc((void **)&g_fz_ctr[dev], alloc));
-        HCHK(hipMemset(g_fz_ctr[dev], 0, alloc));
-        g_fz_bytes[dev] = alloc;
-        if (!g_fz_err_host[dev]) {
-            HCHK(hipHostMalloc((void **)&g_fz_err_host[dev], 64, hipHostMallocDefault));
-            *g_fz_err_host[dev] = 0;
+        HCHK(hipMalloc((void **)&g_pl_ctr[dev], alloc));
+        g_pl_bytes[dev] = alloc;
+        if (!g_pl_err_host[dev]) {
+            HCHK(hipHostMalloc((void **)&g_pl_err_host[dev], 64, hipHostMallocDefault));
+            *g_pl_err_host[dev] = 0;
         }
     }
-    unsigned *ctr = g_fz_ctr[dev];
-    HCHK(hipMemsetAsync(ctr + CS, 0, 2 * CS * (size_t)ng * sizeof(unsigned), stream()));
+    unsigned *ctr = g_pl_ctr[dev];
+    HCHK(hipMemsetAsync(ctr, 0, need, stream()));
     bxc::XArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)in;
@@ -829,6 +727,8 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         a.sleep = e ? (unsigned)atoi(e) : 1u;
         e = getenv("HSFFT_BX_MAP");
         a.xmap = e ? (unsigned)atoi(e) & 1u : 1u;
+        e = getenv("HSFFT_BX_JITTER"); /* uneven-load tests: per-phase delays, results unchanged */
+        a.jitter = e ? (unsigned)atoi(e) : 0u;
     }
     static unsigned *s_dbg = nullptr;
     const char *dbgenv = getenv("HSFFT_BX_DEBUG");
@@ -840,10 +740,12 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
     HCHK(hipGetLastError());
-    HCHK(hipMemcpyAsync(g_fz_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
+    HCHK(hipMemcpyAsync(g_pl_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
+    HCHK(hipStreamSynchronize(stream()));
+    const unsigned err = *(volatile unsigned *)g_pl_err_host[dev];
+    *g_pl_err_host[dev] = 0;
     if (dbg) { /* mean us per row: P1, wait A, P2, wait B, P3 */
         static unsigned h[4096 * 8];
-        HCHK(hipStreamSynchronize(stream()));
         HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
         double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int w = 0; w < grid; w++)
@@ -854,6 +756,10 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
                 "P3 %.2f\n",
                 grid, t[0] / grid, t[1] / rows / 100.0, t[6] / rows / 100.0, t[2] / rows / 100.0, t[3] / rows / 100.0,
                 t[7] / rows / 100.0, t[4] / rows / 100.0, t[5] / rows / 100.0);
+    }
+    if (err) {
+        snprintf(g_err, sizeof g_err, "hsd_blue_xcd: an in-launch wait timed out (error word %u)", err);
+        return 2;
     }
     return 0;
 }
@@ -967,8 +873,6 @@ const char *hsd_errstr(void) { return g_err; }
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
 {
     if (p->variant == HS_KV_R8X3) {
-        const int rw = wl::launch(p, l, stream());
-        if (rw <= 0) return rw;
         const int rc = pf::launch(p, l, stream());
         if (rc <= 0) return rc;
         return r8::launch(p, l, stream());
@@ -1280,7 +1184,7 @@ int hsd_timer_stop(float *ms)
     HCHK(hipEventRecord(g_t1[dev], stream()));
     HCHK(hipEventSynchronize(g_t1[dev]));
     HCHK(hipEventElapsedTime(ms, g_t0[dev], g_t1[dev]));
-    return 0;
+    return pl_check(); /* a timed persistent launch whose waits timed out is an error, not a time */
 }
 
 int hsd_pass_timer_begin(int i)
@@ -1306,7 +1210,7 @@ int hsd_pass_timer_read(int n, float *ms)
         HCHK(hipEventSynchronize(g_pev[dev][2 * i + 1]));
         HCHK(hipEventElapsedTime(&ms[i], g_pev[dev][2 * i], g_pev[dev][2 * i + 1]));
     }
-    return 0;
+    return pl_check();
 }
 
 }  // extern "C"

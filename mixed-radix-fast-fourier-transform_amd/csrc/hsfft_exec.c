@@ -643,7 +643,10 @@ static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long
         l.nt_load |= (nt >> 2) & 1;
         l.nt_store |= (nt >> 3) & 1;
     }
-    if (env_int("HSFFT_DEV_ALIAS", 0) & 1) l.idist = l.odist = 0; /* dev probe: MALL-resident timing only */
+#ifdef HSFFT_DEV_PROBES
+    /* development build only: every row aliased to one buffer (on-die timing, results wrong) */
+    if (env_int("HSFFT_DEV_ALIAS", 0) & 1) l.idist = l.odist = 0;
+#endif
     int rc = hsd_run_pass(&e->pass[i], &l);
     if (rc) hs_seterr("pass %d: %s", i, hsd_errstr());
     return rc;
@@ -678,28 +681,6 @@ static int run_pipelined(hs_entry *e, hs_devstate *ds, const void *I, long long 
     return rc;
 }
 
-/* 2^20 = [4,8,8,8 | 8,8,8] with plain loads/stores and contiguous output rows: both passes
- * in one persistent launch (hsfft_fused.h), pass-B output in place on O */
-static int fused_rows(int batch)
-{
-    const int r = env_int("HSFFT_FZ_R", 2);
-    return (r == 1 || r == 2 || r == 4) && batch % r == 0 ? r : 1;
-}
-
-static int fused20_ok(const hs_entry *e, long long odist, int batch, int load_op, int store_op)
-{
-    if (!env_int("HSFFT_FUSED", 0) || e->M != (1 << 20) || e->npass != 2 || odist != e->M) return 0;
-    if (load_op != HS_LOAD_PLAIN || store_op != HS_STORE_PLAIN || batch < 1) return 0;
-    const hsd_pass *a = &e->pass[0], *b = &e->pass[1];
-    if (a->nst != 4 || !a->leaf || a->B != 1 || a->A != 512 || a->radix[0] != 4) return 0;
-    if (b->nst != 3 || b->B != 2048 || b->A != 1) return 0;
-    for (int s = 1; s < 4; s++)
-        if (a->radix[s] != 8) return 0;
-    for (int s = 0; s < 3; s++)
-        if (b->radix[s] != 8) return 0;
-    return 1;
-}
-
 /* One mixed-radix transform of length M per row, chained over the plan's passes.  Reads
  * I (never written), writes O.  Intermediate buffers come from the scratch pool; the last
  * pass (A == 1: it reads and writes the same element set per tile) may run in place on O
@@ -717,15 +698,6 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     }
     if (n == 1)
         return launch_pass(e, ds, 0, I, idist, O, odist, batch, sgn, conj, dir, load_op, laux, store_op, saux, nsig);
-    if (fused20_ok(e, odist, batch, load_op, store_op)) {
-        const int R = fused_rows(batch);
-        int grid = env_int("HSFFT_FZ_GRID", 0);
-        if (grid <= 0) grid = (hsd_cu_count() > 0 ? hsd_cu_count() : 256) * 2;
-        grid = (grid + 7) / 8 * 8;
-        int rc = hsd_fused20(I, idist, O, odist, ds->d_tw, batch, sgn, conj, R, env_int("HSFFT_FZ_LAG", 2), grid);
-        if (rc) hs_seterr("fused pass: %s", hsd_errstr());
-        return rc;
-    }
     const int last_inplace = store_op != HS_STORE_CHIRP && odist == M;
     /* passes 0..n-2 write scratch except that pass n-2 writes O when the last pass can run
      * in place; consecutive scratch writes alternate between two buffers */
@@ -753,7 +725,11 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     if (!need && n == 2 && chunk < batch && env_int("HSFFT_PIPE", 0))
         return run_pipelined(e, ds, I, idist, O, odist, batch, (int)chunk, sgn, conj, dir, load_op, laux, store_op,
                              saux, nsig);
-    const int dev_np = env_int("HSFFT_DEV_NPASS", 0); /* dev probe: stop after this many passes */
+#ifdef HSFFT_DEV_PROBES
+    const int dev_np = env_int("HSFFT_DEV_NPASS", 0); /* development build only: stop after this many passes */
+#else
+    const int dev_np = 0;
+#endif
     for (long long c0 = 0; c0 < batch; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         const void *R = (const fft_data *)I + c0 * idist;
@@ -780,6 +756,12 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     return 0;
 }
 
+/* persistent Bluestein launches whose rows were re-run on the three-launch path (waits timed
+ * out); read by hsfft_bluestein_fallbacks() */
+static long long g_blue_fallbacks;
+
+long long hsfft_bluestein_fallbacks(void) { return __atomic_load_n(&g_blue_fallbacks, __ATOMIC_RELAXED); }
+
 /* Bluestein (ref :1735-1907) on rows of length N: pre-multiply fused into the first pass of
  * FFT #2, the spectrum product into its last pass, FFT #3 runs with conjugated twiddles and
  * sign -sgn, the post-multiply is fused into its last pass.  hk was computed once per plan. */
@@ -796,26 +778,35 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
     const int fuse = e->npass == 2 && M == 512 * 512 && p0->P == 512 && p1->P == 512 && p0->nst == 3 &&
                      p1->nst == 3 && p0->variant == HS_KV_R8X3 && p1->variant == HS_KV_R8X3 &&
                      p0->radix[0] == 8 && !env_int("HSFFT_BLUE_NOFUSE", 0);
-    /* one persistent launch per call (hsfft_blue_xcd.h): groups of 64 workgroups carry one row
-     * at a time through all three kernels, the intermediates stay on die (HSFFT_BLUE_XCD=0:
-     * three launches per chunk) */
+    /* one persistent launch per 65536 rows (hsfft_blue_xcd.h): groups of 64 workgroups carry
+     * one row at a time through all three kernels, the intermediates stay on die
+     * (HSFFT_BLUE_XCD=0: three launches per chunk).  The launch is synchronous; if its waits
+     * timed out (its workgroups were not all resident), the rows from that launch on run on the
+     * three-launch path below. */
     const int ng = env_int("HSFFT_BLUE_XCD", 8);
+    long long done = 0;
     if (fuse && ng > 0) {
         const size_t ib = (size_t)ng * 4 * sizeof(fft_data) * (size_t)M; /* 4 images per group */
         void *img = hs_scratch(3, ib);
-        /* launches of at most 65536 rows (the in-launch counters stay far from wrapping) */
         int rc = img ? 0 : 1;
         for (long long c0 = 0; c0 < batch && rc == 0; c0 += 65536) {
             const int cb = (int)(batch - c0 < 65536 ? batch - c0 : 65536);
             rc = hsd_blue_xcd((const fft_data *)in + c0 * idist, idist, (fft_data *)out + c0 * odist, odist, ds->d_tw,
                               ds->d_chirp, ds->d_hk, img, ib, N, cb, e->sgn, ng);
-            if (rc == 1 && c0 > 0) rc = -1; /* applicability cannot change between chunks */
+            if (rc == 0) done = c0 + cb;
         }
         if (rc < 0) {
             hs_seterr("bluestein persistent launch: %s", hsd_errstr());
             return HSFFT_ERR_DEVICE;
         }
-        if (rc == 0) return 0;
+        if (rc == 2) __atomic_fetch_add(&g_blue_fallbacks, 1, __ATOMIC_RELAXED);
+        if (done == batch) return 0;
+    }
+    if (done) {
+        in = (const fft_data *)in + done * idist;
+        out = (fft_data *)out + done * odist;
+        batch -= (int)done;
+        if (chunk > batch) chunk = batch;
     }
     /* the two M-point intermediates; halved while the allocation fails (a fuller device runs
      * in smaller chunks) */
@@ -830,9 +821,13 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
         hs_seterr("bluestein scratch allocation of %lld bytes failed", (long long)(chunk * M * 16));
         return HSFFT_ERR_NOMEM;
     }
-    /* HSFFT_DEV_ALIAS bit 1 (timing probe only, results WRONG): every row of a chunk uses the
-     * same M-point intermediate, so the hand-offs between the three kernels stay on die */
+#ifdef HSFFT_DEV_PROBES
+    /* development build only (results WRONG): every row of a chunk uses the same M-point
+     * intermediate, so the hand-offs between the three kernels stay on die */
     const long long md = (env_int("HSFFT_DEV_ALIAS", 0) & 2) ? 0 : M;
+#else
+    const long long md = M;
+#endif
     for (long long c0 = 0; c0 < batch && fuse; c0 += chunk) {
         const int cb = (int)(batch - c0 < chunk ? batch - c0 : chunk);
         int rc = hsd_blue_first((const fft_data *)in + c0 * idist, idist, mid, md, ds->d_tw, ds->d_chirp, N, cb, e->sgn);

@@ -99,7 +99,8 @@ int mr_has_variant(const hsd_pass *p);
  * h+1 bins (hsfft_r2c_batched_compact) instead of the mirrored N */
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
                  long long B, int batch, int sgn, int compact);
-/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h); 1 = not applicable */
+/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h), synchronous: 0 done, 1 not
+ * applicable, 2 in-launch waits timed out (re-run the rows elsewhere), < 0 HIP error */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
                  const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng);
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
@@ -131,9 +132,6 @@ int hsd_scale_real(void *x, long long n, int batch, long long dist, double divis
 int hsd_copy_rows(const void *src, long long sdist, long long soff, long long ncopy, void *dst, long long ddist,
                   long long dlen, int batch);
 
-/* 2^20 = [4,8,8,8 | 8,8,8] as one persistent launch (hsfft_fused.h); rows of 2^20 complex */
-int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
-                int conj, int rows_per_group, int lag, int grid);
 int hsd_cu_count(void);
 
 /* timing on the library stream */

@@ -659,8 +659,8 @@ static const Variant k_variants[] = {
     MRV(2, 7, 8, 1, 1, 8, 45, false, false),
     MRV(2, 7, 8, 1, 1, 8, 15, false, false),
     MRV(2, 7, 8, 1, 1, 8, 16, false, false),
-    /* 12600 whole-row (HSFFT_MR_ROW=0: the two passes above) */
-    {6, {3, 3, 5, 5, 7, 8}, 1024, 1, true, true, k_row<3, 3, 5, 5, 7, 8, 1024>, true},
+    /* 12600 whole-row (HSFFT_MR_ROW=0: the two passes above); launched as k_row2 */
+    {6, {3, 3, 5, 5, 7, 8}, 512, 1, true, true, nullptr, true},
 };
 #undef MRV
 
@@ -703,12 +703,6 @@ inline const Variant *select(hsd_pass *p)
     return best;
 }
 
-inline int env_row_v()
-{
-    const char *e = getenv("HSFFT_ROW_V");
-    return e ? atoi(e) : 2;
-}
-
 inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
 {
     hsd_pass tmp = *p;
@@ -733,44 +727,21 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         const char *e = getenv("HSFFT_MR_XCD");
         a.xcd = e ? atoi(e) : 1; /* c3: 78-80 -> 84-88 GSamples/s */
     }
-    if (v->row && env_row_v() == 2 && v->r[0] == 3 && v->r[1] == 3 && v->r[2] == 5 && v->r[3] == 5 && v->r[4] == 7 &&
-        v->r[5] == 8) {
+    if (v->row) { /* 12600 = [3,3,5,5,7,8]: k_row2 (the only whole-row variant) */
         constexpr int P = 12600, NT = 1574;
-        /* HSFFT_ROW_PRE=1: LDS-DMA prefetch of the next row's first 8448 points into the image
-         * while this row is stored -- bit-exact, measured slower (109 vs 113.6 GSamples/s: the
-         * DMA queues behind the row's stores on the CU's memory path; load phase unchanged) */
-        const char *ep = getenv("HSFFT_ROW_PRE");
-        const bool rpre = ep ? atoi(ep) != 0 : false;
-        const size_t lds = rpre ? (size_t)NT * sizeof(double2) + (size_t)ROW_PRE_PTS * sizeof(double2)
-                                : (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
+        const size_t lds = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
         if (l->batch <= 0) {
             snprintf(g_err, sizeof g_err, "mr: bad row batch=%d", l->batch);
             return -1;
         }
-        const char *ef = getenv("HSFFT_ROW_F01");
-        const bool f01 = ef ? atoi(ef) != 0 : true;
-        kfn fn = f01 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true>)
-                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, false> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, false>);
-        if (rpre)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 1024, true, true, true> : k_row2<3, 3, 5, 5, 7, 8, 1024, false, true, true>;
-        /* default: 512 threads (8 waves, 256 VGPRs per thread) with the next row's first input
-         * group (37 % of the row) loaded into registers during this row's stages 2-5: 113.5 ->
-         * 123.5 GSamples/s; HSFFT_ROW_T=1024 (16 waves, 128 VGPRs: round 1's kernel) / 768 (168
-         * VGPRs) without prefetch, HSFFT_ROW_PF=0 the 512-thread kernel without it.  The
-         * prefetching 768 / 1024-thread kernels (25 / 21 dwords of spill) and the two-group
-         * prefetch (4 dwords, no faster) were measured and removed */
-        const char *et = getenv("HSFFT_ROW_T"), *epf = getenv("HSFFT_ROW_PF");
-        const int rt = et ? atoi(et) : 512, rpf = epf ? atoi(epf) : 1;
-        int threads = 1024;
-        if (f01 && !rpre && rt == 768) {
-            threads = 768;
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 768, true, true> : k_row2<3, 3, 5, 5, 7, 8, 768, false, true>;
-        } else if (f01 && !rpre && rt == 512) { /* 8 waves, 256 VGPRs: room for one group */
-            threads = 512;
-            fn = rpf ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
-                               : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>)
-                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true> : k_row2<3, 3, 5, 5, 7, 8, 512, false, true>);
-        }
+        /* 512 threads (8 waves, 256 VGPRs per thread) with the next row's first input group
+         * (37 % of the row) loaded into registers during this row's stages 2-5: 113.5 -> 123.5
+         * GSamples/s over the 1024-thread kernel.  Measured and removed: 768 /
+         * 1024-thread kernels, prefetching ones that spill, an LDS-DMA prefetch of the next row,
+         * the unfused stage 0/1 form. */
+        const kfn fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
+                              : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>;
+        const int threads = 512;
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));
         HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -798,18 +769,6 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
                     ph[0] / rows / 100, ph[1] / rows / 100, ph[2] / rows / 100, ph[3] / rows / 100, ph[4] / rows / 100,
                     ph[5] / rows / 100, ph[6] / rows / 100, rows);
         }
-        return 0;
-    }
-    if (v->row) {
-        const size_t lds = (size_t)p->P * sizeof(double);
-        if (l->batch <= 0 || lds > 160 * 1024) {
-            snprintf(g_err, sizeof g_err, "mr: bad row geometry batch=%d lds=%zu", l->batch, lds);
-            return -1;
-        }
-        a.tiles = a.tiles_q = 1;
-        HCHK(hipFuncSetAttribute((const void *)v->fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(v->fn, dim3((unsigned)l->batch), dim3(v->tpg), lds, st, a);
-        HCHK(hipGetLastError());
         return 0;
     }
     const long long ext = v->first ? p->A : p->B;

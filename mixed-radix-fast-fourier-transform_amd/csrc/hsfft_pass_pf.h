@@ -114,7 +114,7 @@ __device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, uns
 }
 
 /* stages + exchanges + store of one first-pass tile held in xr/xi; ocol = output column */
-template <int R0, int N8, int G, int SGN, bool CONJ, bool SC1 = false, bool TWG = false>
+template <int R0, int N8, int G, int SGN, bool CONJ, bool TWG = false>
 __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], double2 *lds, const double2 *ltw,
                                            double2 *orow, unsigned m, unsigned jt, unsigned g,
                                            const double2 *gtw = nullptr)
@@ -144,69 +144,7 @@ __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], dou
     /* last stage: output u = jt + jj*LL of the column, written to [m][u] */
     constexpr int LL = S::Lloc(S::NST - 1);
 #pragma unroll
-    for (int jj = 0; jj < 8; jj++) {
-        if constexpr (SC1) { /* write-through for an in-launch consumer (hsfft_fused.h) */
-            typedef unsigned u4 __attribute__((ext_vector_type(4)));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(orow, 0, 0x7fffffff, 0x00020000);
-            const double2 v = make_double2(xr[jj], xi[jj]);
-            u4 u;
-            __builtin_memcpy(&u, &v, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(u, rs, (m * P + jt) * 16u, jj * LL * 16, 16);
-        } else {
-            stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
-        }
-    }
-}
-
-template <int R0, int N8, int G, int TL, int SGN, bool CONJ>
-__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_first(Args a)
-{
-    using S = Shape<R0, N8>;
-    constexpr int P = S::P, TPG = S::TPG, NT = TPG * G;
-    static_assert(N8 >= 1, "leaf-only first passes use k_pass");
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    /* [0, P*G doubles): split exchange image; then tw[0, P): every twiddle a first pass of
-     * P points uses (stage L occupies [L-1, 8L-1), L < P) */
-    double2 *ltw = lds + P * G / 2;
-    const unsigned blk = a.xcd_groups > 0 ? xcd_remap(blockIdx.x) : blockIdx.x;
-    const unsigned groups = (unsigned)a.tiles_q; /* tile groups per row */
-    const unsigned b = blk / groups, tg = blk % groups;
-    const unsigned tid0 = threadIdx.x;
-    const unsigned A = (unsigned)a.A;
-    const unsigned ntiles = A / G;
-
-    const double2 *row = a.in + (long long)b * a.idist;
-    double2 *orow = a.out + (long long)b * a.odist;
-    double pr[8], pi[8];
-    first_load<R0, N8, G>(pr, pi, row, A, tg * G + tid0 % G, tid0 / G);
-#pragma unroll
-    for (int i = tid0; i < P - 1; i += NT) ltw[i] = a.tw[i];
-    __syncthreads();
-    /* straight-line loop body (no branch around the prefetch: a conditional load makes the
-     * waitcnt pass drain vmcnt(0) at the loop header, stores included); the last tile runs
-     * after the loop without a prefetch */
-    const int nit = (int)((ntiles - 1 - tg) / groups + 1); /* tiles tg, tg+groups, ... < ntiles */
-    const unsigned mstep = groups * G;
-#pragma unroll 1
-    for (int it = 0; it < nit - 1; it++) {
-        unsigned tid = tid0;
-        asm volatile("" : "+v"(tid));
-        const unsigned g = tid % G, jt = tid / G;
-        const unsigned m = (tg + it * groups) * G + g;
-        double xr[8], xi[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            xr[i] = pr[i];
-            xi[i] = pi[i];
-        }
-        first_load<R0, N8, G>(pr, pi, row, A, m + mstep, jt);
-        first_body<R0, N8, G, SGN, CONJ>(xr, xi, lds, ltw, orow, m, jt, g);
-    }
-    {
-        const unsigned g = tid0 % G, jt = tid0 / G;
-        const unsigned m = (tg + (nit - 1) * groups) * G + g;
-        first_body<R0, N8, G, SGN, CONJ>(pr, pi, lds, ltw, orow, m, jt, g);
-    }
+    for (int jj = 0; jj < 8; jj++) stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
 }
 
 /* ------------------------------------------------------------------ first pass, paired loads
@@ -284,8 +222,8 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
             yr[k] = pair_swap<G>(oth.x);
             yi[k] = pair_swap<G>(oth.y);
         }
-        first_body<R0, N8, G, SGN, CONJ, false, TWG>(xr, xi, lds, ltw, orow, m0 + h, jt, h, a.tw);
-        first_body<R0, N8, G, SGN, CONJ, false, TWG>(yr, yi, lds, ltw, orow, m0 + G + h, jt, h, a.tw);
+        first_body<R0, N8, G, SGN, CONJ, TWG>(xr, xi, lds, ltw, orow, m0 + h, jt, h, a.tw);
+        first_body<R0, N8, G, SGN, CONJ, TWG>(yr, yi, lds, ltw, orow, m0 + G + h, jt, h, a.tw);
     }
 }
 
@@ -293,7 +231,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
  * P = 512 at L = B (A == 1): input [t][q] (t < 512, q < B), output [u][q].  A workgroup
  * owns 8 adjacent q-columns (128-B rows) and walks T rows of the batch; all three stages'
  * twiddles (k = q + B*kloc) are row-independent: stages 0/1 as LDS runs, stage 2 in
- * registers.  Row prefetch (PREF) is opt-in: it costs the VGPRs that make the kernel spill. */
+ * registers. */
 /* stages + exchanges + store of one [8,8,8] tile-row; ocol = output row + q */
 template <int SGN, bool NTS = false>
 __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], const double2 (&w2)[7], double2 *lds,
@@ -318,7 +256,7 @@ __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], cons
     }
 }
 
-template <int T, int SGN, bool CONJ, bool PREF = true>
+template <int T, int SGN, bool CONJ>
 __global__ __launch_bounds__(512, 4) void k_b512(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -334,17 +272,6 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     const unsigned q0 = tile * G;
     const unsigned b0 = bg * T, nb = (unsigned)a.batch;
 
-    double pr[8], pi[8];
-    if constexpr (PREF) {
-        const double2 *row = a.in + (long long)b0 * a.idist;
-        const unsigned lane = ((tid0 / G) * B + q0 + tid0 % G) * 16u;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const double2 v = ldg(row + (size_t)i * TPG * B, lane);
-            pr[i] = v.x;
-            pi[i] = v.y;
-        }
-    }
     /* stage-2 twiddles (k = q + B*k_local, k_local < 64): coalesced runs redistributed
      * through this wave's slice of the image, kept in registers for all T rows */
     double2 w2[7];
@@ -364,51 +291,24 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
     }
     __syncthreads();
 
+    /* no row prefetch: measured 22.8 ms with it off (106 VGPRs) vs 23.4 ms with it on (128
+     * VGPRs + 40 B of spill) per 4096 x 2^20 */
     const int nit = (int)min((unsigned)T, nb - b0);
-    if constexpr (!PREF) { /* no row prefetch: 32 fewer VGPRs (no scratch spill) */
 #pragma unroll 1
-        for (int it = 0; it < nit; it++) {
-            unsigned tid = tid0;
-            asm volatile("" : "+v"(tid));
-            const unsigned g = tid % G, jt = tid / G;
-            const unsigned b = b0 + it, lane = (jt * B + q0 + g) * 16u;
-            const double2 *row = a.in + (long long)b * a.idist;
-            double xr[8], xi[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const double2 v = ldg(row + (size_t)i * TPG * B, lane);
-                xr[i] = v.x;
-                xi[i] = v.y;
-            }
-            b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
-        }
-        return;
-    }
-#pragma unroll 1
-    for (int it = 0; it < nit - 1; it++) {
+    for (int it = 0; it < nit; it++) {
         unsigned tid = tid0;
         asm volatile("" : "+v"(tid));
         const unsigned g = tid % G, jt = tid / G;
         const unsigned b = b0 + it, lane = (jt * B + q0 + g) * 16u;
+        const double2 *row = a.in + (long long)b * a.idist;
         double xr[8], xi[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            xr[i] = pr[i];
-            xi[i] = pi[i];
-        }
-        const double2 *row = a.in + (long long)(b + 1) * a.idist;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
             const double2 v = ldg(row + (size_t)i * TPG * B, lane);
-            pr[i] = v.x;
-            pi[i] = v.y;
+            xr[i] = v.x;
+            xi[i] = v.y;
         }
         b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
-    }
-    {
-        const unsigned g = tid0 % G, jt = tid0 / G;
-        const unsigned b = b0 + nit - 1, lane = (jt * B + q0 + g) * 16u;
-        b512_body<SGN>(pr, pi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
     }
 }
 
@@ -423,7 +323,6 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
  * Saves the c2c output's write and re-read (16 of 56 bytes per real sample). */
 /* one tile's row loads, its stage-0/1 twiddle runs (-> ltw) and stage-2 twiddles (coalesced,
  * redistributed through the image: every earlier reader of the image must be done) */
-template <int PROBE = 0>
 __device__ __forceinline__ void r2c_load(double (&xr)[8], double (&xi)[8], double2 (&w2)[7], const double2 *row,
                                          unsigned B, unsigned q0, const double2 *tw, double2 *lds, double2 *ltw,
                                          unsigned tid0)
@@ -432,31 +331,21 @@ __device__ __forceinline__ void r2c_load(double (&xr)[8], double (&xi)[8], doubl
     const unsigned lane0 = ((tid0 >> 3) * B + q0 + (tid0 & 7)) * 16u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        if constexpr (PROBE & 8) { /* timing probe: no data loads */
-            xr[i] = (double)(lane0 + i);
-            xi[i] = (double)(q0 - i);
-        } else {
-            const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
-            xr[i] = v.x;
-            xi[i] = v.y;
-        }
+        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
+        xr[i] = v.x;
+        xi[i] = v.y;
     }
     r8::Args ta;
     ta.tw = tw;
     ta.B = B;
-    if constexpr (PROBE & 2) { /* timing probe: no stage-2 twiddle loads (wrong results) */
-#pragma unroll
-        for (int i = 0; i < 7; i++) w2[i] = make_double2(1.0, 0.0);
-    } else {
-        r8::load_tw_co<64>(w2, ta, (int)(tid0 >> 3), q0);
-    }
+    r8::load_tw_co<64>(w2, ta, (int)(tid0 >> 3), q0);
     __syncthreads(); /* earlier readers of the image and of ltw are done */
     if (tid0 < 504) {
         const unsigned r = tid0 / 56, e = tid0 % 56;
         const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
         ltw[tid0] = tw[src];
     }
-    if constexpr (!(PROBE & 2)) r8::redistribute_tw(w2, lds);
+    r8::redistribute_tw(w2, lds);
     __syncthreads(); /* ltw written; every wave has read its redistributed twiddles back */
 }
 
@@ -481,10 +370,7 @@ __device__ __forceinline__ void r2c_stages(double (&xr)[8], double (&xi)[8], con
     stage<8, SGN>(xr, xi, w2, false);
 }
 
-/* PROBE (timing only, HSFFT_R2C_PROBE; results WRONG): bit 0 twiddle2 not loaded, bit 1
- * stage-2 twiddles not loaded, bit 2 no output stores, bit 3 no data loads -- what each
- * stream costs */
-template <int SGN, bool COMPACT, int PROBE = 0>
+template <int SGN, bool COMPACT>
 __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -503,9 +389,9 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
     if (j < tiles - 1) {
         const unsigned qlo = 8 * j + 1, qhi = B - 8 * j - 8;
         double hr[8], hi[8];
-        r2c_load<PROBE>(hr, hi, w2, row, B, qhi, a.tw, lds, ltw, tid0);
+        r2c_load(hr, hi, w2, row, B, qhi, a.tw, lds, ltw, tid0);
         r2c_stages<SGN, false>(hr, hi, w2, lds, ltw, tid0);
-        r2c_load<PROBE>(xr, xi, w2, row, B, qlo, a.tw, lds, ltw, tid0);
+        r2c_load(xr, xi, w2, row, B, qlo, a.tw, lds, ltw, tid0);
         /* the hi tile's real parts wait in the image's upper half (the lo tile's split
          * exchanges use the lower half), so only its imaginary parts stay in registers */
 #pragma unroll
@@ -522,26 +408,15 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
             const unsigned s = (P - 1 - u) * G + (7 - g);
             const double2 zk = make_double2(xr[jj], xi[jj]), zh = make_double2(ld[4096 + s], ld[s]);
             double re, im;
-            r8::r2c_pair(zk, zh, (PROBE & 1) ? make_double2(1.0, 0.0) : w2t[k], re, im);
-            const bool st = !(PROBE & 4) || re == -7.25e300; /* PROBE bit 2: no stores */
-            /* bit 4: no stores to the line-straddling streams X[k], X[h+k]; bit 5: none to the
-             * aligned X[N-k], X[h-k] */
-            const bool sm = st && (!(PROBE & 16) || re == -7.25e300), sa = st && (!(PROBE & 32) || re == -7.25e300);
-            /* bit 6: non-temporal output stores */
-#define R2C_ST(idx, v)                                  \
-    do {                                                \
-        if (PROBE & 64) stg_nt(X, (idx) * 16u, (v));    \
-        else X[idx] = (v);                              \
-    } while (0)
-            if (sm) R2C_ST(k, make_double2(re, im));
-            if (!COMPACT && sa) R2C_ST(N - k, make_double2(re, -im));
-            r8::r2c_pair(zh, zk, (PROBE & 1) ? make_double2(1.0, 0.0) : w2t[hk], re, im);
-            if (sa || re == -7.25e300) R2C_ST(hk, make_double2(re, im));
-            if (!COMPACT && (sm || re == -7.25e300)) R2C_ST(N - hk, make_double2(re, -im));
-#undef R2C_ST
+            r8::r2c_pair(zk, zh, w2t[k], re, im);
+            X[k] = make_double2(re, im);
+            if (!COMPACT) X[N - k] = make_double2(re, -im);
+            r8::r2c_pair(zh, zk, w2t[hk], re, im);
+            X[hk] = make_double2(re, im);
+            if (!COMPACT) X[N - hk] = make_double2(re, -im);
         }
     } else { /* column 0: k = u*B pairs with (P-u)*B */
-        r2c_load<PROBE>(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
+        r2c_load(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
         r2c_stages<SGN, false>(xr, xi, w2, lds, ltw, tid0);
         __syncthreads();
 #pragma unroll
@@ -566,198 +441,12 @@ __global__ __launch_bounds__(512, 4) void k_r2c_fused(Args a, unsigned h)
     }
 }
 
-/* ------------------------------------------------------------------ r2c split, tile walk
- * Same split and arithmetic as k_r2c_fused, rearranged so that every output line is written
- * whole.  Why: the lo tile's columns [8j+1, 8j+9) put the X[k] and X[h+k] streams one entry
- * off the 128-B lines (7 entries in line j, 1 in line j+1), and a line written in two parts by
- * two workgroups costs ~3x an aligned one (tools/experiments/r2c_stores.hip: 4 streams, no
- * arithmetic, 10.5 ms per 512 rows with two such streams, 5.3 ms with all four aligned).
- * Here a 1024-thread workgroup walks T consecutive tile pairs j of one row: threads [0, 512)
- * transform the lo tile and threads [512, 1024) the hi tile at the same time (one exchange
- * image each), each half computes its own half of the pair outputs (lo: X[k], X[N-k]; hi:
- * X[h-k], X[h+k]), and the two off-line streams are shifted by one lane within each 8-lane
- * group before the store: the entry that falls into line j+1 is carried (LDS, same thread)
- * to the next tile's store, so each store instruction writes eight whole 128-B lines.  Only
- * the first line of a walk (its entry 0 belongs to the previous walk) and the carry left at
- * the end are partial.  Reference layout only (rows of N bins); the last walk WG of a row
- * index W handles column 0. */
-__device__ __forceinline__ void r2cw_load(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned B, unsigned q0,
-                                          unsigned t)
-{
-    constexpr int TPG = 64;
-    const unsigned lane0 = ((t >> 3) * B + q0 + (t & 7)) * 16u;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
-        xr[i] = v.x;
-        xi[i] = v.y;
-    }
-}
-
-/* the tile's twiddles (stage-0/1 runs -> ltw, stage-2 coalesced + redistributed) and its
- * three stages; the tile's points are in xr/xi (loaded earlier, possibly still in flight) */
-template <int SGN>
-__device__ __forceinline__ void r2cw_tile(double (&xr)[8], double (&xi)[8], unsigned B, unsigned q0,
-                                          const double2 *tw, double2 *img, double2 *ltw, unsigned t)
-{
-    constexpr int P = 512, G = 8;
-    double2 w2[7];
-    {
-        r8::Args ta;
-        ta.tw = tw;
-        ta.B = B;
-        r8::load_tw_co<64>(w2, ta, (int)(t >> 3), q0);
-    }
-    __syncthreads(); /* the previous tile's readers of both images and of ltw are done */
-    if (t < 504) {
-        const unsigned r = t / 56, e = t % 56;
-        const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
-        ltw[t] = tw[src];
-    }
-    { /* r8::redistribute_tw with the wave index inside this half */
-        const unsigned lane = t & 63, wave = t >> 6;
-        double2 *reg = img + wave * 448 + (lane >> 3) * 56;
-#pragma unroll
-        for (int j = 0; j < 7; j++) reg[(lane & 7) + 8 * j] = w2[j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int i = 0; i < 7; i++) w2[i] = reg[(lane & 7) * 7 + i];
-    }
-    __syncthreads(); /* ltw written; every wave has read its twiddles back from the image */
-    r2c_stages<SGN, false>(xr, xi, w2, img, ltw, t);
-    (void)P;
-    (void)G;
-}
-
 /* lane (g-1) of this 8-lane group (DIR = -1) or lane (g+1) (DIR = +1), wrapping in the group */
 template <int DIR>
 __device__ __forceinline__ double2 grp_shift(double2 v)
 {
     const int lane = __lane_id(), src = (lane & ~7) | ((lane + DIR) & 7);
     return make_double2(__shfl(v.x, src, 64), __shfl(v.y, src, 64));
-}
-
-constexpr int R2CW_LDS = (2 * 4096 + 2 * 504 + 1024) * 16; /* 2 images, 2 twiddle runs, 2 carry rows */
-
-template <int SGN>
-__global__ __launch_bounds__(1024, 1) void k_r2c_walk(Args a, unsigned h, unsigned T, unsigned W)
-{
-    constexpr int P = 512, TPG = 64, G = 8;
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    const unsigned blk = xcd_remap(blockIdx.x), b = blk / (W + 1), s = blk % (W + 1);
-    const unsigned tid = threadIdx.x, half = tid >> 9, t = tid & 511, g = t & 7, jt = t >> 3;
-    double2 *img = lds + half * 4096, *pimg = lds + (half ^ 1) * 4096;
-    double2 *ltw = lds + 8192 + half * 504, *cry = lds + 8192 + 2 * 504 + half * 512;
-    const unsigned B = (unsigned)a.B, N = 2 * h;
-    const double2 *row = a.in + (long long)b * a.idist;
-    double2 *X = a.out + (long long)b * a.odist;
-    const double2 *w2t = a.saux;
-    double xr[8], xi[8];
-    if (s == W) { /* column 0 (k = u*B pairs with (P-u)*B): both halves transform the tile, the lo half writes */
-        r2cw_load(xr, xi, row, B, 0, t);
-        r2cw_tile<SGN>(xr, xi, B, 0, a.tw, img, ltw, t);
-        __syncthreads();
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) img[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
-        __syncthreads();
-        if (half || g != 0) return;
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) {
-            const unsigned u = jt + jj * TPG, k = u * B;
-            const double2 zk = make_double2(xr[jj], xi[jj]);
-            if (u == 0) {
-                X[0] = make_double2(zk.x + zk.y, 0.0);
-                X[h] = make_double2(zk.x - zk.y, 0.0);
-            } else {
-                const double2 zh = img[(P - u) * G];
-                double re, im;
-                r8::r2c_pair(zk, zh, w2t[k], re, im);
-                X[k] = make_double2(re, im);
-                X[N - k] = make_double2(re, -im);
-            }
-        }
-        return;
-    }
-    const unsigned j0 = s * T, j1 = min(j0 + T, B / 16);
-    /* HSFFT_R2C_DEBUG: per-workgroup phase clock in a.laux (thread 0, 100 MHz ticks):
-     * [0] twiddles + stages (incl. the data wait), [1] image write + barrier, [2] pairs + stores */
-    unsigned *dbg = (unsigned *)a.laux, tp = 0;
-#define R2CW_MARK(i)                                                              \
-    if (dbg && tid == 0) {                                                        \
-        const unsigned tn = (unsigned)__builtin_amdgcn_s_memrealtime();           \
-        dbg[blockIdx.x * 4 + (i)] += tn - tp;                                     \
-        tp = tn;                                                                  \
-    }
-    if (dbg && tid == 0) tp = (unsigned)__builtin_amdgcn_s_memrealtime();
-    r2cw_load(xr, xi, row, B, half ? B - 8 * j0 - 8 : 8 * j0 + 1, t);
-#pragma unroll 1
-    for (unsigned j = j0; j < j1; j++) {
-        const unsigned q0 = half ? B - 8 * j - 8 : 8 * j + 1;
-        r2cw_tile<SGN>(xr, xi, B, q0, a.tw, img, ltw, t);
-        if (dbg) {
-            r8::pin(xr);
-            R2CW_MARK(0)
-        }
-        /* the last exchange ended with a barrier: both images are free */
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) img[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
-        __syncthreads();
-        R2CW_MARK(1)
-        /* the next tile's points load while this tile's pairs are formed and stored (the pair
-         * loop reads this tile's points back from the image) */
-        {   /* unconditional (the last tile reloads itself): a branch around the loads makes the
-             * waitcnt pass drain vmcnt at the join */
-            const unsigned jn = j + 1 < j1 ? j + 1 : j;
-            r2cw_load(xr, xi, row, B, half ? B - 8 * jn - 8 : 8 * jn + 1, t);
-        }
-        const bool first = j == j0;
-#pragma unroll 2
-        for (int jj = 0; jj < 8; jj++) {
-            const unsigned u = jt + jj * TPG, k = u * B + q0 + g; /* this thread's bin */
-            const double2 z = img[(jt + jj * TPG) * G + g], zp = pimg[(P - 1 - u) * G + (7 - g)];
-            double re, im;
-            r8::r2c_pair(z, zp, w2t[k], re, im);
-            if (!half) {
-                /* X[N-k] (aligned); X[k] = bins 8j+1+g -> line [8j, 8j+8) takes lane g-1's value,
-                 * lane 0 the entry carried from the previous tile (bin 8j) */
-                X[N - k] = make_double2(re, -im);
-                const double2 v = grp_shift<-1>(make_double2(re, im)); /* lane 0: lane 7's = next carry */
-                const unsigned p = u * B + 8 * j + g;
-                if (g != 0) X[p] = v;
-                else {
-                    if (!first) X[p] = cry[u];
-                    cry[u] = v;
-                }
-            } else {
-                /* X[h-k] = this bin (aligned); X[h+k'] (k' = the lo partner, bins 8j+8-g of row
-                 * P-1-u) -> line [8j, 8j+8) written descending: lane g takes lane g+1's value,
-                 * lane 7 the carried entry (bin 8j) */
-                X[k] = make_double2(re, im);
-                const double2 v = grp_shift<1>(make_double2(re, -im)); /* lane 7: lane 0's = next carry */
-                const unsigned p = h + (P - 1 - u) * B + 8 * j + 7 - g;
-                if (g != 7) X[p] = v;
-                else {
-                    if (!first) X[p] = cry[u];
-                    cry[u] = v;
-                }
-            }
-        }
-        R2CW_MARK(2)
-        if (dbg && tid == 0) dbg[blockIdx.x * 4 + 3] += 1;
-    }
-#undef R2CW_MARK
-    /* the carry of the last tile: bin 8*j1 of the off-line streams (already written by the
-     * other stream's aligned stores when j1 is the row's last tile: column B/2) */
-    if (j1 < B / 16 && j1 > j0) {
-#pragma unroll
-        for (int jj = 0; jj < 8; jj++) {
-            const unsigned u = jt + jj * TPG;
-            if (!half && g == 0) X[u * B + 8 * j1] = cry[u];
-            if (half && g == 7) X[h + (P - 1 - u) * B + 8 * j1] = cry[u];
-        }
-    }
 }
 
 /* ------------------------------------------------------------------ r2c split, 512-thread walk
@@ -938,12 +627,9 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     a.B = B;
     a.batch = batch;
     a.tiles = a.tiles_q = B / 16 + 1;
-    /* whole-line tile walk (opt-in, HSFFT_R2C_WALK=1): bit-exact, but one 1024-thread workgroup
-     * per CU loses more overlap than the aligned stores gain (c5 95.4 vs 98.2 GSamples/s) */
     /* default: k_r2c_walk2, 32 tile pairs per walk (c5 98.4 -> 100.6-101.4 GSamples/s);
-     * HSFFT_R2C_WALK=0: k_r2c_fused, =1: k_r2c_walk */
-    const int walk = env("HSFFT_R2C_WALK", 2);
-    if (!compact && walk == 2 && !getenv("HSFFT_R2C_PROBE")) { /* 512-thread walk */
+     * HSFFT_R2C_WALK=0 (and the compact layout): k_r2c_fused */
+    if (!compact && env("HSFFT_R2C_WALK", 2) != 0) {
         const long long T = env("HSFFT_R2C_WT", 32) > 0 ? env("HSFFT_R2C_WT", 32) : 32, W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
@@ -954,58 +640,11 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         HCHK(hipGetLastError());
         return 0;
     }
-    if (!compact && walk == 1 && !getenv("HSFFT_R2C_PROBE")) {
-        const long long T = env("HSFFT_R2C_WT", 16) > 0 ? env("HSFFT_R2C_WT", 16) : 16, W = (B / 16 + T - 1) / T;
-        const long long grid = (W + 1) * (long long)batch;
-        if (grid <= 0 || grid > 0x7fffffffLL) return -1;
-        void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk<1> : k_r2c_walk<-1>;
-        HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW_LDS));
-        static unsigned *s_dbg = nullptr;
-        const bool dbg = env("HSFFT_R2C_DEBUG", 0) && grid <= (1 << 20);
-        if (dbg) {
-            if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, (size_t)(1 << 20) * 4 * sizeof(unsigned)));
-            HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 4 * sizeof(unsigned), st));
-            a.laux = (const double2 *)s_dbg;
-        }
-        hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(1024), R2CW_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
-        HCHK(hipGetLastError());
-        if (dbg) {
-            unsigned *hb = (unsigned *)malloc((size_t)grid * 4 * sizeof(unsigned));
-            HCHK(hipStreamSynchronize(st));
-            HCHK(hipMemcpy(hb, s_dbg, (size_t)grid * 4 * sizeof(unsigned), hipMemcpyDeviceToHost));
-            double ph[4] = {0, 0, 0, 0};
-            for (long long i = 0; i < grid; i++)
-                for (int k = 0; k < 4; k++) ph[k] += hb[i * 4 + k];
-            free(hb);
-            const double n = ph[3] > 0 ? ph[3] : 1;
-            fprintf(stderr, "k_r2c_walk per tile pair (us): twiddles+stages %.2f  image+barrier %.2f  pairs+stores %.2f | steps %.0f\n",
-                    ph[0] / n / 100, ph[1] / n / 100, ph[2] / n / 100, n);
-        }
-        return 0;
-    }
     const long long grid = a.tiles * (long long)batch;
     if (grid <= 0 || grid > 0x7fffffffLL) return -1;
     const size_t lds = (size_t)(512 * 8 + 504) * sizeof(double2);
     void (*fn)(Args, unsigned) = compact ? (sgn == 1 ? k_r2c_fused<1, true> : k_r2c_fused<-1, true>)
                                          : (sgn == 1 ? k_r2c_fused<1, false> : k_r2c_fused<-1, false>);
-    {
-        const char *pe = getenv("HSFFT_R2C_PROBE");
-        const int pr = pe ? atoi(pe) & 127 : 0;
-        if (sgn == 1 && !compact) switch (pr) {
-            case 1: fn = k_r2c_fused<1, false, 1>; break;
-            case 2: fn = k_r2c_fused<1, false, 2>; break;
-            case 3: fn = k_r2c_fused<1, false, 3>; break;
-            case 4: fn = k_r2c_fused<1, false, 4>; break;
-            case 7: fn = k_r2c_fused<1, false, 7>; break;
-            case 8: fn = k_r2c_fused<1, false, 8>; break;
-            case 12: fn = k_r2c_fused<1, false, 12>; break;
-            case 15: fn = k_r2c_fused<1, false, 15>; break;
-            case 16: fn = k_r2c_fused<1, false, 16>; break;
-            case 32: fn = k_r2c_fused<1, false, 32>; break;
-            case 64: fn = k_r2c_fused<1, false, 64>; break;
-            default: break;
-            }
-    }
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), lds, st, a, (unsigned)h);
     HCHK(hipGetLastError());
@@ -1021,22 +660,9 @@ inline int env(const char *name, int dflt)
     return s ? atoi(s) : dflt;
 }
 
-template <int R0, int N8, int G, int TL>
-inline kfn first_fn(int sgn, int conj)
-{
-    if (sgn == 1) return conj ? k_first<R0, N8, G, TL, 1, true> : k_first<R0, N8, G, TL, 1, false>;
-    return conj ? k_first<R0, N8, G, TL, -1, true> : k_first<R0, N8, G, TL, -1, false>;
-}
-
 template <int T>
 inline kfn b512_fn(int sgn, int conj)
 {
-    /* default: no row prefetch -- 106 VGPRs, no scratch; 22.8 vs 23.4 ms with the prefetch
-     * (128 VGPRs + 40 B spill), i.e. the pass runs at the stream-copy rate */
-    if (!env("HSFFT_PFB_PREF", 0)) {
-        if (sgn == 1) return conj ? k_b512<T, 1, true, false> : k_b512<T, 1, false, false>;
-        return conj ? k_b512<T, -1, true, false> : k_b512<T, -1, false, false>;
-    }
     if (sgn == 1) return conj ? k_b512<T, 1, true> : k_b512<T, 1, false>;
     return conj ? k_b512<T, -1, true> : k_b512<T, -1, false>;
 }
@@ -1052,34 +678,17 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
     for (int s = 1; s < p->nst; s++)
         if (p->radix[s] != 8) return nullptr;
     if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 4) { /* 2^20's pass A: [4,8,8,8] */
-        /* default k_firstq walking 4 column groups: 24.0-24.3 ms per 4096 x 2^20 against
-         * 27.0-27.2 for k_first<G=2,T=2> (HSFFT_PFQ=0 selects k_first) */
-        const int q = env("HSFFT_PFQ", 4);
-        if (q > 0 && p->A % 4 == 0) { /* 64-B loads: *G = 4 columns per tile for the grid */
+        /* k_firstq walking 4 column groups: 24.0-24.3 ms per 4096 x 2^20 against 27.0-27.2 for
+         * its 32-B-segment predecessor k_first (round 1; removed in round 3) */
+        if (p->A % 4 == 0) { /* 64-B loads: *G = 4 columns per tile for the grid */
             *G = 4;
-            *TL = q;
+            *TL = env("HSFFT_PFQ", 4) > 0 ? env("HSFFT_PFQ", 4) : 4;
             *threads = 512;
             *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
             if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 2, 1, true> : k_firstq<4, 3, 2, 1, false>;
             return l->conj ? k_firstq<4, 3, 2, -1, true> : k_firstq<4, 3, 2, -1, false>;
         }
-        const int g = env("HSFFT_PFG", 2), t = env("HSFFT_PFT", 2); /* T=2: same time as 8, fabric reads 73.6 vs 103 GB */
-        if (p->A % g) return nullptr;
-        *threads = 256 * g;
-        *lds = (size_t)2048 * g * sizeof(double) + 2048 * sizeof(double2);
-        *G = g;
-        if (g == 1) *TL = t >= 8 ? 8 : 4;
-        else if (g == 2) *TL = t >= 8 ? 8 : t >= 4 ? 4 : 2;
-        else if (g == 4) *TL = t >= 4 ? 4 : t >= 2 ? 2 : 1;
-        else return nullptr;
-        if (g == 1) return *TL == 8 ? first_fn<4, 3, 1, 8>(l->sgn, l->conj) : first_fn<4, 3, 1, 4>(l->sgn, l->conj);
-        if (g == 2)
-            return *TL == 8 ? first_fn<4, 3, 2, 8>(l->sgn, l->conj)
-                 : *TL == 4 ? first_fn<4, 3, 2, 4>(l->sgn, l->conj)
-                            : first_fn<4, 3, 2, 2>(l->sgn, l->conj);
-        return *TL == 4 ? first_fn<4, 3, 4, 4>(l->sgn, l->conj)
-             : *TL == 2 ? first_fn<4, 3, 4, 2>(l->sgn, l->conj)
-                        : first_fn<4, 3, 4, 1>(l->sgn, l->conj);
+        return nullptr;
     }
     if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 8 && p->A % 2 == 0) {
         /* [8,8,8,8] first pass (2^21 = r2c 2^22's inner pass A): 32-B paired loads, one column
@@ -1141,8 +750,6 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         snprintf(g_err, sizeof g_err, "pf: bad grid %lld", grid);
         return -1;
     }
-    /* dev probe: HSFFT_PF_OCC1=1 pads the dynamic LDS so only one workgroup fits per CU */
-    if (env("HSFFT_PF_OCC1", 0)) lds = lds > 100 * 1024 ? lds : 100 * 1024;
     if (lds > 65536) {
         hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return set_err(e, "hipFuncSetAttribute");

@@ -66,6 +66,7 @@ SIGNATURES = {
     "hsfft_time_r2c_batched": (CI, [VP, VP, VP, CI, CI, ctypes.POINTER(ctypes.c_float)]),
     "hsfft_exec_multi": (CI, [VP, VP, VP, CI, CI]),
     "hsfft_bench_copy": (CI, [VP, VP, ctypes.c_size_t, CI, ctypes.POINTER(ctypes.c_float)]),
+    "hsfft_bluestein_fallbacks": (ctypes.c_longlong, []),
 }
 
 STRUCT_TWIDDLE_OFFSET = 272  # offsetof(struct fft_set, twiddle), include/highspeedFFT.h

@@ -221,13 +221,6 @@ int hsd_copy_rows(const void *src, long long sdist, long long soff, long long nc
     touch_rows_w(dst, ddist, dlen, batch, 8);
     return 0;
 }
-int hsd_fused20(const void *in, long long idist, void *out, long long odist, const void *tw, int batch, int sgn,
-                int conj, int rows_per_group, int lag, int grid)
-{
-    touch_rows_r(in, idist, 1 << 20, batch, 16);
-    touch_rows_w(out, odist, 1 << 20, batch, 16);
-    return 0;
-}
 int hsd_timer_start(void) { return 0; }
 int hsd_copy_bench(const void *src, void *dst, long long n16, int iters, float *ms)
 {

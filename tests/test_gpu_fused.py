@@ -1,13 +1,15 @@
-"""GPU parity of the 2^20 hot-path kernel families (BASELINE config 2) against the oracle:
+"""GPU parity of the hot-path kernel families against the oracle:
 
-* pf::k_firstq / pf::k_first / pf::k_b512 (csrc/hsfft_pass_pf.h): the two-launch passes
-  (64-B quad-load first pass, its 32-B predecessor, the row-looped later pass);
-* fz::k_fused (csrc/hsfft_fused.h): both passes in one persistent launch with the
-  intermediate handed over inside the launch (HSFFT_FUSED=1).
+* pf::k_firstq / pf::k_b512 (csrc/hsfft_pass_pf.h): the two passes of 2^20 (BASELINE config
+  2) and the [8,8,8,8] first pass of 2^21 (config 5's inner c2c);
+* bxc::k_bxcd (csrc/hsfft_blue_xcd.h): Bluestein M = 2^18 (config 4) as one persistent launch
+  with in-launch hand-offs, checked on small odd batches, under uneven load (per-phase
+  random delays) and at the FULL config-4 size on every output word;
+* bpf::k_bfirst / k_bmid / k_blast (csrc/hsfft_blue_pf.h): the three-launch Bluestein path
+  (the persistent launch's fallback).
 
 Tolerance: bit-exact (0 ulp) against the oracle (the CPU restatement pinned to the reference)
-and against the two-launch path.  Batch sizes cover a partial last row group, a single row
-(R falls back to 1), every rows-per-group setting and lags larger than the group count.
+and against the other schedules of the same transform.
 """
 import numpy as np
 import pytest
@@ -54,23 +56,14 @@ def _oracle(x, sgn, key):
     return _cache[k]
 
 
-@pytest.mark.parametrize("pf,pfq", [("0", "4"), ("1", "4"), ("2", "4"), ("3", "4"), ("3", "0")])
-def test_pipelined_passes_bit_exact(pf, pfq, monkeypatch):
+@pytest.mark.parametrize("pf", ["0", "1", "2", "3"])
+def test_pipelined_passes_bit_exact(pf, monkeypatch):
+    """HSFFT_PF bit 0: pf::k_firstq for pass A, bit 1: pf::k_b512 for pass B (else the
+    register kernels of hsfft_pass_r8.h)"""
     monkeypatch.setenv("HSFFT_PF", pf)
-    monkeypatch.setenv("HSFFT_PFQ", pfq)
     x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
     for sgn in (1, -1):
         assert T.bits_equal(_run(x, sgn), _oracle(x, sgn, "b3")), (pf, sgn)
-
-
-@pytest.mark.parametrize("g,t", [(1, 8), (2, 2), (2, 8), (4, 4)])
-def test_pipelined_first_pass_tiles(g, t, monkeypatch):
-    monkeypatch.setenv("HSFFT_PF", "1")
-    monkeypatch.setenv("HSFFT_PFQ", "0")
-    monkeypatch.setenv("HSFFT_PFG", str(g))
-    monkeypatch.setenv("HSFFT_PFT", str(t))
-    x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
-    assert T.bits_equal(_run(x, 1), _oracle(x, 1, "b3"))
 
 
 @pytest.mark.parametrize("q", ["1", "2", "3"])
@@ -104,45 +97,6 @@ def test_paired_load_first_pass_2p21(pfp, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("batch,r,lag", [(1, 2, 2), (2, 2, 2), (6, 2, 2), (8, 4, 1), (5, 1, 3), (6, 2, 9)])
-def test_fused_bit_exact(batch, r, lag, monkeypatch):
-    monkeypatch.setenv("HSFFT_FUSED", "1")
-    monkeypatch.setenv("HSFFT_FZ_R", str(r))
-    monkeypatch.setenv("HSFFT_FZ_LAG", str(lag))
-    x = T.complex_input(N, 0xF00D ^ batch, batch=batch).reshape(batch, N)
-    for sgn in (1, -1):
-        y = _run(x, sgn)
-        ref = _oracle(x, sgn, ("f", batch))
-        assert T.bits_equal(y, ref), (batch, r, lag, sgn, T.mismatches(y, ref))
-
-
-@pytest.mark.parametrize("mode", ["1"])
-def test_fused_large_batch_vs_two_launch(mode, monkeypatch):
-    """64 rows (16 GiB of pass traffic): the fused launch equals the two-launch path bit for
-    bit on every row and the oracle on sampled rows; no dependency wait timed out."""
-    batch = 64
-    p = hsfft.Plan(N, 1)
-    din = hsfft.DeviceBuffer(batch * N * 16)
-    d2 = hsfft.DeviceBuffer(batch * N * 16)
-    d1 = hsfft.DeviceBuffer(batch * N * 16)
-    hsfft.fill_complex(din, batch * N, T.SEEDS[2])
-    monkeypatch.setenv("HSFFT_FUSED", "0")
-    hsfft.exec_batched(p, din, d2, batch)
-    hsfft.synchronize()
-    monkeypatch.setenv("HSFFT_FUSED", mode)
-    d1.fill_zero()
-    hsfft.exec_batched(p, din, d1, batch)
-    hsfft.synchronize()
-    a = d1.to_array(np.complex128)
-    b = d2.to_array(np.complex128)
-    assert T.bits_equal(a, b)
-    for row in (0, 37, batch - 1):
-        x = T.complex_input(N, T.SEEDS[2], batch=1, row0=row)
-        assert T.bits_equal(a[row * N:(row + 1) * N], T.oracle_c2c(x, 1)), row
-    for d in (din, d1, d2):
-        d.free()
-
-
 @pytest.mark.parametrize("n,batch,chunk_mb", [(1 << 20, 7, "32"), (4096, 33, "1"), (12600, 5, "1"), (99991, 3, "2")])
 def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
     """hsfft_exec_batched_host (host rows streamed through HBM in chunks, upload / transform /
@@ -155,18 +109,16 @@ def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("mask,t,pref", [("0", "4", "0"), ("3", "1", "0"), ("3", "2", "0"), ("3", "4", "0"), ("3", "8", "0"),
-                                         ("7", "8", "1"), ("1", "4", "0"), ("2", "4", "0")])
+@pytest.mark.parametrize("mask,xt", [("0", "3"), ("7", "0"), ("7", "3"), ("7", "7"), ("1", "3"), ("2", "3"), ("4", "3")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
-def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
+def test_bluestein_row_looped_kernels(n, mask, xt, monkeypatch):
     """Bluestein with M = 2^18 (config 4's size; 65537 = 2^16+1 is the plan/exec M mismatch
-    case D5, computed with its own exec-length table): the row-looped middle / last kernels
-    (csrc/hsfft_blue_pf.h) for every tile-row count, odd batch, both signs, bit-exact."""
+    case D5, computed with its own exec-length table): the row-looped first / middle / last
+    kernels (csrc/hsfft_blue_pf.h, HSFFT_BLUE_PF mask; the generic passes otherwise), both
+    block orders, odd batch (a partial 8-row group), both signs, bit-exact."""
     monkeypatch.setenv("HSFFT_BLUE_XCD", "0")  # the three-launch path
     monkeypatch.setenv("HSFFT_BLUE_PF", mask)
-    monkeypatch.setenv("HSFFT_BLUE_T", t)
-    monkeypatch.setenv("HSFFT_BLUE_PREF", pref)
-    monkeypatch.setenv("HSFFT_BLUE_XT", "0" if t == "2" else "3")  # both block orders
+    monkeypatch.setenv("HSFFT_BLUE_XT", xt)
     x = T.complex_input(n, 0xB1 ^ n, batch=5).reshape(5, n)
     for sgn in (1, -1):
         p = hsfft.Plan(n, sgn)
@@ -175,20 +127,24 @@ def test_bluestein_row_looped_kernels(n, mask, t, pref, monkeypatch):
         hsfft.exec_batched(p, din, dout, 5)
         hsfft.synchronize()
         y = dout.to_array(np.complex128).reshape(5, n)
-        assert T.bits_equal(y, _oracle(x, sgn, ("blue", n))), (n, sgn, mask, t)
+        assert T.bits_equal(y, _oracle(x, sgn, ("blue", n))), (n, sgn, mask, xt)
         din.free()
         dout.free()
         p.close()
 
 
-@pytest.mark.parametrize("ng,batch", [("8", 1), ("8", 5), ("8", 19), ("3", 7), ("1", 2)])
+@pytest.mark.parametrize("ng,batch,jitter", [("8", 1, "0"), ("8", 5, "0"), ("8", 19, "0"), ("3", 7, "0"), ("1", 2, "0"),
+                                             ("8", 19, "3"), ("3", 7, "5")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
-def test_bluestein_persistent_launch(n, ng, batch, monkeypatch):
+def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
     """Bluestein M = 2^18 as one persistent launch (csrc/hsfft_blue_xcd.h: groups of 64
     workgroups carry a row through the three passes, intermediates handed over in-launch):
-    fewer rows than groups, ragged last round, both signs -- bit-exact vs the oracle and vs
-    the three-launch path."""
+    fewer rows than groups, ragged last round, both signs, and under uneven load (HSFFT_BX_JITTER:
+    pseudo-random per-phase delays scramble the hand-off order) -- bit-exact vs the oracle and
+    vs the three-launch path; no launch fell back."""
     monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
+    monkeypatch.setenv("HSFFT_BX_JITTER", jitter)
+    fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
     x = T.complex_input(n, 0xB7 ^ n ^ batch, batch=batch).reshape(batch, n)
     for sgn in (1, -1):
         p = hsfft.Plan(n, sgn)
@@ -207,6 +163,46 @@ def test_bluestein_persistent_launch(n, ng, batch, monkeypatch):
         din.free()
         dout.free()
         p.close()
+    assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
+
+
+@pytest.mark.parametrize("jitter", ["0", "2"])
+def test_bluestein_persistent_full_size_every_word(jitter, monkeypatch):
+    """BASELINE config 4 at full size (99991 x 8192) through the persistent launch, compared on
+    EVERY output word with the three-launch path (no in-launch hand-off), plus sampled rows vs
+    the oracle.  jitter 2 runs it under uneven load (random per-phase delays of 0-2 units).
+    The persistent launch reuses each image every two rows, so its consumers read lines their
+    CU read before (L1-warm), as MI355X_MICROARCH.md asks hand-off tests to do."""
+    n, batch = 99991, 8192
+    monkeypatch.setenv("HSFFT_BX_JITTER", jitter)
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer(batch * n * 16)
+    d1 = hsfft.DeviceBuffer(batch * n * 16)
+    d2 = hsfft.DeviceBuffer(batch * n * 16)
+    hsfft.fill_complex(din, batch * n, T.SEEDS[4])
+    fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "8")
+    hsfft.exec_batched(p, din, d1, batch)
+    hsfft.synchronize()
+    assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0, "the persistent launch fell back"
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "0")
+    hsfft.exec_batched(p, din, d2, batch)
+    hsfft.synchronize()
+    rows = 256  # compared in chunks of 256 rows (410 MB per buffer)
+    bad = 0
+    for r0 in range(0, batch, rows):
+        off = r0 * n * 16
+        a = d1.to_array(np.complex128, rows * n, off)
+        b = d2.to_array(np.complex128, rows * n, off)
+        bad += int((a.view(np.uint64) != b.view(np.uint64)).sum())
+    assert bad == 0, f"{bad} 8-byte words differ between the persistent and the three-launch path"
+    for row in (0, 4097, batch - 1):
+        x = T.complex_input(n, T.SEEDS[4], batch=1, row0=row)
+        y = d1.to_array(np.complex128, n, row * n * 16)
+        assert T.bits_equal(y, _oracle(x, 1, ("c4row", row))), row
+    for d in (din, d1, d2):
+        d.free()
+    p.close()
 
 
 @pytest.mark.parametrize("fuse", ["0", "1"])

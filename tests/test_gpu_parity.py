@@ -585,22 +585,19 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wt", ["16", "1", "5", "4096", "walk0", "w2:16", "w2:1", "w2:5", "w2:4096"])
+@pytest.mark.parametrize("wt", ["walk0", "w2:16", "w2:1", "w2:5", "w2:4096"])
 @pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
 def test_r2c_walk(n, sgn, wt, monkeypatch):
-    """pf::k_r2c_walk (opt-in split kernel of the reference-layout r2c): walks of WT tile pairs
-    per workgroup, whole-line stores with the one-entry carry between tiles.  WT=1: every tile
-    is a walk's first (partial first line, carry written at once); 5: walks of uneven length
-    and a short last walk; 4096: one walk per row (the carry reaches column B/2); walk0: the
-    one-tile-per-workgroup k_r2c_fused.  Bit-exact vs the oracle, odd batch."""
+    """pf::k_r2c_walk2 (default split kernel of the reference-layout r2c): walks of WT tile
+    pairs per workgroup, whole-line stores with the one-entry carry between tiles.  WT=1: every
+    tile is a walk's first (partial first line, carry written at once); 5: walks of uneven
+    length and a short last walk; 4096: one walk per row (the carry reaches column B/2);
+    walk0: the one-tile-per-workgroup k_r2c_fused.  Bit-exact vs the oracle, odd batch."""
     if wt == "walk0":
         monkeypatch.setenv("HSFFT_R2C_WALK", "0")
-    elif wt.startswith("w2:"):
+    else:
         monkeypatch.setenv("HSFFT_R2C_WALK", "2")
         monkeypatch.setenv("HSFFT_R2C_WT", wt[3:])
-    else:
-        monkeypatch.setenv("HSFFT_R2C_WALK", "1")
-        monkeypatch.setenv("HSFFT_R2C_WT", wt)
     x = T.real_input(n, 29, batch=3).reshape(3, n)
     rp = hsfft.RealPlan(n, sgn)
     din = hsfft.DeviceBuffer.from_array(x)
@@ -612,19 +609,16 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F01": "0"}, {"HSFFT_ROW_V": "1"}, {"HSFFT_MR_ROW": "0"},
-                                 {"HSFFT_ROW_T": "1024", "HSFFT_ROW_PRE": "1"}, {"HSFFT_ROW_T": "1024"},
-                                 {"HSFFT_ROW_T": "768"}, {"HSFFT_ROW_T": "512", "HSFFT_ROW_PF": "0"}])
+@pytest.mark.parametrize("env", [{}, {"HSFFT_MR_ROW": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     """config 3's schedules, bit-exact vs the oracle, both signs: 300 rows leave the
     row-walking grid uneven (300 rows over 256 workgroups); 64 rows give every workgroup
     exactly ONE row, so no row can lean on an earlier row's barriers (the stage-1 twiddles of
-    the fused first stages are read right after the per-workgroup LDS copy).  Variants:
+    the fused first stages are read right after the per-workgroup LDS copy).  Schedules:
     mr::k_row2 (default: 512 threads, the next row's first input group prefetched into
-    registers) with 1024 / 768 threads, without the prefetch, stages 0-1 unfused,
-    mr::k_row (one workgroup per row), the two mixed-radix passes, the LDS-DMA prefetch."""
+    registers) and the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600

@@ -19,15 +19,30 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "mixed-radix-fast-fourier-transform_amd", "lib", "libhsfft.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
-# (kernel-name regex on the mangled name, max VGPR spill dwords)
+# (kernel-name regex on the mangled name, max VGPR spill dwords, max VGPRs, min waves per SIMD
+#  that the register allocation allows -- the occupancy each kernel's launch geometry assumes)
 BUDGETS = [
-    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]EE", 0),  # 2^20 pass A (c2)
-    (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]ELb0E", 0),  # 2^20 pass B (c2)
-    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]EE", 0),  # 2^21 pass A (c5)
-    (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0),  # r2c split (c5)
-    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1E", 0),  # 12600 row (c3)
-    (r"^_ZN3bxc6k_bxcdILin?1ELb0E", 8),  # persistent Bluestein (c4): 8 dwords, intrinsic
+    # 2^20 pass A (c2): 512 threads, 2 workgroups per CU need 4 waves per SIMD
+    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]EE", 0, 128, 4),
+    # 2^20 pass B (c2)
+    (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]EE", 0, 112, 4),
+    # 2^21 pass A (c5)
+    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]EE", 0, 128, 4),
+    # r2c split walk (c5): one 512-thread workgroup per CU with up to 256 VGPRs
+    (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0, 256, 2),
+    # 12600 row kernel (c3): one 512-thread workgroup per CU
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1E", 0, 256, 2),
+    # persistent Bluestein (c4): the whole grid (2 workgroups per CU) must be resident, so
+    # 128 VGPRs is a hard limit; 8 dwords of spill are intrinsic (also compiled alone)
+    (r"^_ZN3bxc6k_bxcdILin?1EE", 8, 128, 4),
 ]
+
+
+def waves_per_simd(vgprs):
+    """register-limited waves per SIMD on gfx950: allocation granule 8, 512 registers per lane
+    (MI355X_MICROARCH.md, Register files)"""
+    alloc = max(8, -(-vgprs // 8) * 8)
+    return min(8, 512 // alloc)
 
 
 def _metadata():
@@ -54,7 +69,7 @@ def _metadata():
             cur = m.group(1)
             kernels.setdefault(cur, {})
             continue
-        m = re.match(r"\s+\.(vgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\d+)", line)
+        m = re.match(r"\s+\.(vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|sgpr_count):\s+(\d+)", line)
         if m and cur:
             kernels[cur][m.group(1)] = int(m.group(2))
     return kernels
@@ -62,8 +77,32 @@ def _metadata():
 
 def test_hot_kernels_do_not_spill():
     kernels = _metadata()
-    for pat, cap in BUDGETS:
+    for pat, cap, _, _ in BUDGETS:
         hits = {k: v for k, v in kernels.items() if re.match(pat, k)}
         assert hits, f"no kernel matches {pat}"
         for name, res in hits.items():
             assert res.get("vgpr_spill_count", 0) <= cap, (name, res)  # SGPR spills go to VGPR lanes: cheap
+
+
+def test_hot_kernels_register_allocation():
+    """VGPR count (VGPR + AGPR: one file on gfx950) within budget, and the occupancy it allows
+    at least what the launch geometry assumes -- a register-allocation change in a hot kernel
+    fails here even without a spill"""
+    kernels = _metadata()
+    for pat, _, vmax, wmin in BUDGETS:
+        hits = {k: v for k, v in kernels.items() if re.match(pat, k)}
+        assert hits, f"no kernel matches {pat}"
+        for name, res in hits.items():
+            regs = res.get("vgpr_count", 0) + res.get("agpr_count", 0)
+            assert regs <= vmax, (name, res, vmax)
+            assert waves_per_simd(regs) >= wmin, (name, res, wmin)
+
+
+def test_no_wrong_result_probes_in_product():
+    """the timing probes that compute wrong results exist only in the development build
+    (-DHSFFT_DEV_PROBES): the product library must not even contain their names"""
+    if not os.path.exists(LIB):
+        pytest.skip("lib/libhsfft.so not built")
+    blob = open(LIB, "rb").read()
+    for probe in (b"HSFFT_DEV_ALIAS", b"HSFFT_DEV_NPASS", b"HSFFT_R2C_PROBE", b"HSFFT_BX_PLAIN", b"HSFFT_BLUE_PROBE"):
+        assert probe not in blob, probe
