@@ -264,42 +264,64 @@ def bench_c1(args, comm, ws, rank):
                       "parallelism": "replicas only"},
            "latency_us": {"p10": round(lat[len(lat) // 10] * 1e6, 2), "median": round(med_us, 2),
                           "p90": round(lat[len(lat) * 9 // 10] * 1e6, 2)}}
-    ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
-    if rank == 0 and os.path.exists(ref_so) and not args.no_cpu_baseline:
-        R = ctypes.CDLL(ref_so)
-        R.hsref_time_batch_reps.restype = ctypes.c_double
-        R.hsref_time_batch_reps.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, ctypes.c_int]
-        reps = 200000
-        secs = R.hsref_time_batch_reps(n, 1, 0, 1, 1, seed, reps)
-        out["cpu_baseline"] = {"value": round(secs / reps * 1e6, 3), "unit": "us", "cores": 1, "kind": "reference",
-                               "sample": f"{reps} back-to-back fft_exec calls of N={n} on one core, {secs:.2f} s"}
+    if rank == 0 and not args.no_cpu_baseline:
+        cb = c1_cpu_baseline(seed)
+        if cb:
+            out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
     dx.free()
 
 
-def other_configs(steps=3, warmup=1):
-    """The other BASELINE configs, each at its full per-GPU workload, timed in the same run
-    as the headline (one rank): wall time over `steps` steps between device synchronisations,
-    inputs generated in HBM.  c1 is the median latency of single host-buffer fft_exec calls."""
+def c1_latency(iters=300, warmup=20):
+    """median latency of one N=1024 forward c2c fft_exec on host buffers (drop-in API)"""
     import numpy as np
-    out = {}
     L = hsfft.lib()
-    # c1: one N=1024 transform on host buffers
     p1 = hsfft.Plan(1024, 1)
     x = np.ascontiguousarray(np.exp(1j * np.arange(1024.0)))
     y = np.zeros_like(x)
     px, py = x.ctypes.data_as(ctypes.c_void_p), y.ctypes.data_as(ctypes.c_void_p)
-    for _ in range(20):
+    for _ in range(warmup):
         L.fft_exec(p1.ptr, px, py)
     lat = []
-    for _ in range(300):
+    for _ in range(iters):
         t = time.perf_counter()
         L.fft_exec(p1.ptr, px, py)
         lat.append(time.perf_counter() - t)
     lat.sort()
-    out["c1"] = {"value": round(lat[len(lat) // 2] * 1e6, 2), "unit": "us", "workload": CONFIGS["c1"][4]}
     p1.close()
+    return lat
+
+
+def c1_cpu_baseline(seed=0x5EED0001, reps=200000):
+    """the reference's fft_exec for N=1024 on ONE host core (its own single-thread design)"""
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
+    if not os.path.exists(ref_so):
+        return None
+    R = ctypes.CDLL(ref_so)
+    R.hsref_time_batch_reps.restype = ctypes.c_double
+    R.hsref_time_batch_reps.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, ctypes.c_int]
+    secs = R.hsref_time_batch_reps(1024, 1, 0, 1, 1, seed, reps)
+    return {"value": round(secs / reps * 1e6, 3), "unit": "us", "cores": 1, "kind": "reference",
+            "sample": f"{reps} back-to-back fft_exec calls of N=1024 on one core, {secs:.2f} s"}
+
+
+def other_configs(steps=10, warmup=2, cpu=True, cpu_seconds=8.0):
+    """The other BASELINE configs, each at its full per-GPU workload, timed in the same run as
+    the headline (one rank): `steps` steps between HIP events on the library stream after
+    `warmup` untimed ones (the wall clock of the same steps is reported beside), inputs
+    generated in HBM; each with its roofline fraction, its PMC traffic (profiles/
+    pmc_traffic.json, when measured at this batch) and the reference timed on the host cores
+    over a bounded sample (`cpu_seconds` per config).  c1 is the median latency of single
+    host-buffer fft_exec calls beside the reference on one core."""
+    out = {}
+    lat = c1_latency()
+    out["c1"] = {"value": round(lat[len(lat) // 2] * 1e6, 2), "unit": "us", "workload": CONFIGS["c1"][4],
+                 "higher_is_better": False, "steps": len(lat),
+                 "latency_us": {"p10": round(lat[len(lat) // 10] * 1e6, 2), "p90": round(lat[len(lat) * 9 // 10] * 1e6, 2)}}
+    if cpu:
+        out["c1"]["cpu_baseline"] = c1_cpu_baseline()
+    L = hsfft.lib()
     for name in ("c3", "c4", "c5"):
         kind, n, batch, seed, desc = CONFIGS[name]
         if kind == "c2c":
@@ -307,6 +329,7 @@ def other_configs(steps=3, warmup=1):
             din, dout = hsfft.DeviceBuffer(n * batch * 16), hsfft.DeviceBuffer(n * batch * 16)
             hsfft.fill_complex(din, n * batch, seed, 0)
             run = lambda: hsfft.exec_batched(plan, din, dout, batch)  # noqa: E731
+            timed = lambda k: hsfft.time_batched(plan, din, dout, batch, k)[0]  # noqa: E731
         else:
             plan = hsfft.RealPlan(n, 1)
             chunk = min(batch, max(1, (64 << 30) // (n * 16)))
@@ -317,6 +340,13 @@ def other_configs(steps=3, warmup=1):
                 for c0 in range(0, batch, chunk):
                     hsfft.check(L.hsfft_r2c_batched(plan.ptr, ctypes.c_void_p(din.ptr + c0 * n * 8),
                                                     ctypes.c_void_p(dout.ptr), min(chunk, batch - c0)), "r2c")
+
+            def timed(k):  # every chunk of the step, `k` steps, event-timed per chunk call
+                tot = 0.0
+                for c0 in range(0, batch, chunk):
+                    sub = hsfft.DeviceView(din, c0 * n * 8)
+                    tot += hsfft.time_r2c_batched(plan, sub, dout, min(chunk, batch - c0), k)
+                return tot
         for _ in range(warmup):
             run()
         hsfft.synchronize()
@@ -324,14 +354,25 @@ def other_configs(steps=3, warmup=1):
         for _ in range(steps):
             run()
         hsfft.synchronize()
-        ms = (time.perf_counter() - t0) / steps * 1e3
+        wall_ms = (time.perf_counter() - t0) / steps * 1e3
+        ev_ms = timed(steps) / steps
         bps = 32 if kind == "c2c" else 24
-        out[name] = {"value": round(n * batch / (ms / 1e3) / 1e9, 3), "unit": "GSamples/s", "ms_per_step": round(ms, 3),
-                     "steps": steps, "frac": round(n * batch * bps / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        alg = n * batch * bps
+        ach = alg / (ev_ms / 1e3) / 1e9
+        ent = traffic_entry(name)
+        out[name] = {"value": round(n * batch / (ev_ms / 1e3) / 1e9, 3), "unit": "GSamples/s",
+                     "ms_per_step": round(ev_ms, 3), "wall_ms_per_step": round(wall_ms, 3), "steps": steps,
+                     "warmup": warmup, "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": read_traffic(name, batch),
+                                  "algorithmic_bytes": alg,
+                                  "kernel": (ent.get("kernel", "") or "").replace("void ", "") or None},
                      "workload": desc}
         din.free()
         dout.free()
         plan.close()
+        if cpu:
+            out[name]["cpu_baseline"] = cpu_baseline(CONFIGS[name], seconds_target=cpu_seconds)
     return out
 
 
@@ -584,7 +625,7 @@ def main():
     if ws == 1 and args.config == "c2" and not args.batch and not args.n and not args.no_other_configs:
         din.free()
         dout.free()
-        out["other_configs"] = other_configs()
+        out["other_configs"] = other_configs(cpu=not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(out), flush=True)
     din.free()

@@ -432,6 +432,129 @@ __device__ __forceinline__ void xchg1_f01(double *x, double *ld, int jt)
     }
 }
 
+/* Two consecutive combine stages fused in registers (k_row2 F23): stage a (radix RA, local L)
+ * and stage b (radix RB, local L*RA).  Group g (< NG2 = P/(RA*RB)) is (ml' = g / L, kloc =
+ * g % L): stage-a butterflies ml' + i'*S' (S' = NG2/L, i' < RB) at kloc and stage-b
+ * butterflies kloc + jj*L (jj < RA) at ml' -- closed under both stages (stage-b butterfly jj
+ * takes output jj of every stage-a butterfly of the group), so the exchange between the two
+ * stages disappears.  Same twiddles (LDS copy, transposed as rstage<TR>), skips and operand
+ * order as the unfused stages, so the results are bit-identical.
+ * Register layout: group c of this thread at x[c*Q ...], point i of stage-a butterfly i' at
+ * x[c*Q + i'*RA + i] on entry; on exit output jj' of stage-b butterfly jj at x[c*Q + jj*RB + jj']. */
+template <int RA, int RB, int L, int P, int TPG, bool CONJ>
+__device__ __forceinline__ void fused_ab(double *xr, double *xi, const double2 *ltw, int jt, int sgn)
+{
+    constexpr int Q = RA * RB, NG2 = P / Q, NGT = cdiv(NG2, TPG), LB = L * RA;
+    const double2 *twa = ltw + (L - 1), *twb = ltw + (LB - 1);
+#pragma unroll
+    for (int c = 0; c < NGT; c++) {
+        int g = c * TPG + jt;
+        if (NGT * TPG != NG2 && g >= NG2) g = NG2 - 1; /* idle slot: compute on a valid group */
+        const unsigned kloc = (unsigned)g % (unsigned)L;
+        double *yr = xr + c * Q, *yi = xi + c * Q;
+        /* stage a: RB butterflies of radix RA, all at k = kloc */
+        {
+            const bool skip = (RA == 4 || RA == 5 || RA == 7) && kloc == 0;
+            double2 t[RA - 1];
+#pragma unroll
+            for (int i = 1; i < RA; i++) t[i - 1] = twa[(i - 1) * L + kloc];
+#pragma unroll
+            for (int ib = 0; ib < RB; ib++) {
+                if (!skip) {
+#pragma unroll
+                    for (int i = 1; i < RA; i++)
+                        hsb::twmul(yr[ib * RA + i], yi[ib * RA + i], t[i - 1].x, CONJ ? -t[i - 1].y : t[i - 1].y);
+                }
+                hsb::bfly<RA>(&yr[ib * RA], &yi[ib * RA], sgn, false);
+            }
+        }
+        /* stage b: butterfly jj (k = kloc + jj*L) takes output jj of stage-a butterfly ib */
+        double zr[Q], zi[Q];
+#pragma unroll
+        for (int jj = 0; jj < RA; jj++) {
+#pragma unroll
+            for (int ib = 0; ib < RB; ib++) {
+                zr[jj * RB + ib] = yr[ib * RA + jj];
+                zi[jj * RB + ib] = yi[ib * RA + jj];
+            }
+            const unsigned k = kloc + (unsigned)jj * L;
+            const bool skip = (RB == 4 || RB == 5 || RB == 7) && k == 0;
+            if (!skip) {
+#pragma unroll
+                for (int i = 1; i < RB; i++) {
+                    const double2 t = twb[(i - 1) * LB + k];
+                    hsb::twmul(zr[jj * RB + i], zi[jj * RB + i], t.x, CONJ ? -t.y : t.y);
+                }
+            }
+            hsb::bfly<RB>(&zr[jj * RB], &zi[jj * RB], sgn, false);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            yr[q] = zr[q];
+            yi[q] = zi[q];
+        }
+    }
+}
+
+/* exchange fused01's outputs (stage-1 butterfly (ml, kloc) output jj at ml*Q0 + kloc + jj*R0)
+ * into fused_ab's group inputs (point i of stage-a butterfly i' of group g at g + NG2*(i' + RB*i)) */
+template <int R0, int R1, int RA, int RB, int P, int TPG>
+__device__ __forceinline__ void xchg1_f01_ab(double *x, double *ld, int jt)
+{
+    constexpr int S = P / (R0 * R1), NG = cdiv(S, TPG), Q0 = R0 * R1;
+    constexpr int Q = RA * RB, NG2 = P / Q, NGT = cdiv(NG2, TPG);
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+        const int ml = g * TPG + jt;
+        if (NG * TPG != S && ml >= S) continue;
+#pragma unroll
+        for (int kloc = 0; kloc < R0; kloc++)
+#pragma unroll
+            for (int jj = 0; jj < R1; jj++) ld[ml * Q0 + kloc + jj * R0] = x[g * Q0 + kloc * R1 + jj];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NGT; c++) {
+        int g = c * TPG + jt;
+        if (NGT * TPG != NG2 && g >= NG2) g = NG2 - 1;
+#pragma unroll
+        for (int ib = 0; ib < RB; ib++)
+#pragma unroll
+            for (int i = 0; i < RA; i++) x[c * Q + ib * RA + i] = ld[g + NG2 * (ib + RB * i)];
+    }
+}
+
+/* exchange fused_ab's outputs (output jj' of stage-b butterfly kloc + jj*L of group (ml', kloc)
+ * at ml'*L*RA*RB + kloc + jj*L + jj'*L*RA) into the next stage's inputs (radix RN at local
+ * LN = L*RA*RB: butterfly b reads (b/LN + i*SN)*LN + b%LN, SN = P/(LN*RN)) */
+template <int RA, int RB, int L, int RN, int P, int TPG>
+__device__ __forceinline__ void xchg1_ab_std(double *x, double *ld, int jt)
+{
+    constexpr int Q = RA * RB, NG2 = P / Q, NGT = cdiv(NG2, TPG), LN = L * Q;
+    constexpr int NBF2 = P / RN, NB2 = cdiv(NBF2, TPG), SN = P / (LN * RN);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NGT; c++) {
+        const int g = c * TPG + jt;
+        if (NGT * TPG != NG2 && g >= NG2) continue;
+        const int mlp = g / L, kloc = g % L;
+#pragma unroll
+        for (int jj = 0; jj < RA; jj++)
+#pragma unroll
+            for (int jq = 0; jq < RB; jq++) ld[mlp * LN + kloc + jj * L + jq * L * RA] = x[c * Q + jj * RB + jq];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NB2; c++) {
+        int b = c * TPG + jt;
+        if (NB2 * TPG != NBF2 && b >= NBF2) b = NBF2 - 1;
+        const int ml = b / LN, kloc = b % LN;
+#pragma unroll
+        for (int i = 0; i < RN; i++) x[c * RN + i] = ld[(ml + i * SN) * LN + kloc];
+    }
+}
+
 /* fused01 for a row whose points [0, 2*P/R0) were prefetched into `pre` by LDS-DMA (k_row2
  * PRE): the remaining leaf inputs (i = R0-1) are loaded from global first, then one barrier
  * behind every wave's vmcnt(0) (all LDS-DMA has landed), then the prefetched inputs are read
@@ -516,14 +639,17 @@ constexpr int ROW_PRE_PTS = 8448;
 /* PF: the inputs of the next row's first PF 9-point groups (37 % of a row per group at
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
-template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0>
+template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
+          bool F23 = false>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(PF == 0 || (F01 && !PRE), "PF prefetches fused01's first groups");
+    static_assert(!F23 || (F01 && !PRE), "F23 follows fused01");
     using LS = List6<R0, R1, R2, R3, R4, R5>;
     constexpr int P = LS::P, NT = LS::Lloc(5) - 1; /* LDS twiddles tw[0, NT) */
     constexpr int NM0 = LS::template nmax<TPG>(), NMF = cdiv(P / (R0 * R1), TPG) * R0 * R1;
-    constexpr int NM = F01 && NMF > NM0 ? NMF : NM0;
+    constexpr int NM1 = F01 && NMF > NM0 ? NMF : NM0, NM23 = cdiv(P / (R2 * R3), TPG) * R2 * R3;
+    constexpr int NM = F23 && NM23 > NM1 ? NM23 : NM1;
     extern __shared__ __attribute__((aligned(16))) double ldsd[];
     /* PRE: [ltw | exchange image + prefetch area]; else [exchange image | ltw] */
     static_assert(!PRE || (F01 && NT % 2 == 0 && 2 * NT * 8 + ROW_PRE_PTS * 16 <= 160 * 1024 &&
@@ -573,8 +699,13 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
                 r8::pin(*reinterpret_cast<double(*)[8]>(xr));
                 mark(a, tp, 0); /* loads + stages 0-1 */
             }
-            xchg1_f01<R0, R1, R2, P, TPG>(xr, img, jt);
-            xchg1_f01<R0, R1, R2, P, TPG>(xi, img, jt);
+            if constexpr (F23) {
+                xchg1_f01_ab<R0, R1, R2, R3, P, TPG>(xr, img, jt);
+                xchg1_f01_ab<R0, R1, R2, R3, P, TPG>(xi, img, jt);
+            } else {
+                xchg1_f01<R0, R1, R2, P, TPG>(xr, img, jt);
+                xchg1_f01<R0, R1, R2, P, TPG>(xi, img, jt);
+            }
             if constexpr (PF > 0) { /* unconditional: the last row of a workgroup reloads itself */
                 const unsigned bn = b + gridDim.x < (unsigned)a.batch ? b + gridDim.x : b;
                 f01_load0<R0, R1, P, TPG, PF>(p0, a.in + (long long)bn * a.idist, jt);
@@ -600,12 +731,20 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             rstage<R1, LS::Lloc(1), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
             xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, img, jt);
         }
-        rstage<R2, LS::Lloc(2), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
-        xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, img, jt);
-        mark(a, tp, 2);
-        rstage<R3, LS::Lloc(3), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
-        xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, img, jt);
-        mark(a, tp, 3);
+        if constexpr (F23) { /* stages 2 and 3 fused in registers: one exchange fewer */
+            fused_ab<R2, R3, LS::Lloc(2), P, TPG, CONJ>(xr, xi, ltw, jt, sgn);
+            mark(a, tp, 2);
+            xchg1_ab_std<R2, R3, LS::Lloc(2), R4, P, TPG>(xr, img, jt);
+            xchg1_ab_std<R2, R3, LS::Lloc(2), R4, P, TPG>(xi, img, jt);
+            mark(a, tp, 3);
+        } else {
+            rstage<R2, LS::Lloc(2), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(2) - 1), jt, sgn);
+            xchg_split<R2, LS::Lloc(2), R3, P, TPG>(xr, xi, img, jt);
+            mark(a, tp, 2);
+            rstage<R3, LS::Lloc(3), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(3) - 1), jt, sgn);
+            xchg_split<R3, LS::Lloc(3), R4, P, TPG>(xr, xi, img, jt);
+            mark(a, tp, 3);
+        }
         rstage<R4, LS::Lloc(4), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(4) - 1), jt, sgn);
         xchg_split<R4, LS::Lloc(4), R5, P, TPG>(xr, xi, img, jt);
         mark(a, tp, 4);
@@ -739,8 +878,14 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * GSamples/s over the 1024-thread kernel.  Measured and removed: 768 /
          * 1024-thread kernels, prefetching ones that spill, an LDS-DMA prefetch of the next row,
          * the unfused stage 0/1 form. */
-        const kfn fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
-                              : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>;
+        /* F23 (HSFFT_ROW_F23, default 1): stages 2 and 3 ([5,5], 504 groups of 25 points)
+         * fused in registers as stages 0 and 1 are -- three exchanges per row instead of four */
+        const char *e23 = getenv("HSFFT_ROW_F23");
+        const bool f23 = e23 ? atoi(e23) != 0 : true;
+        const kfn fn = f23 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true>
+                                     : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true>)
+                           : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
+                                     : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>);
         const int threads = 512;
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));

@@ -219,6 +219,14 @@ class DeviceBuffer:
             pass
 
 
+class DeviceView:
+    """a byte offset into a DeviceBuffer (not owning; never freed)"""
+
+    def __init__(self, buf, offset_bytes):
+        self.ptr = buf.ptr + int(offset_bytes)
+        self.nbytes = buf.nbytes - int(offset_bytes)
+
+
 def exec_batched(plan, d_in, d_out, batch):
     return check(lib().hsfft_exec_batched(plan.ptr, VP(d_in.ptr), VP(d_out.ptr), batch), "exec_batched")
 

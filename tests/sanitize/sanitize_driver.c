@@ -168,6 +168,21 @@ int main(void)
     run_conv(1000, 1000);
     run_conv(1 << 16, 1000);
 
+    /* the persistent Bluestein launch times out (its workgroups were not all resident): the
+     * rows are re-run on the three-launch path and the fallback is counted */
+    {
+        extern int null_bx_timeout;
+        const long long fb0 = hsfft_bluestein_fallbacks();
+        null_bx_timeout = 1;
+        run_c2c(99991, 3);
+        null_bx_timeout = 0;
+        /* run_c2c: 2 signs x (fft_exec, hsfft_exec_batched, hsfft_exec_batched_host) */
+        const long long fb1 = hsfft_bluestein_fallbacks();
+        CHECK(fb1 == fb0 + 6, "bluestein fallback count %lld", fb1 - fb0);
+        run_c2c(99991, 2);
+        CHECK(hsfft_bluestein_fallbacks() == fb1, "no fallback without a timeout");
+    }
+
     /* a caller edits the public fields between calls: the registry rebuilds its entry */
     fft_object e = fft_init(64, 1);
     fft_data *x = cbuf(64), *y = cbuf(64);
