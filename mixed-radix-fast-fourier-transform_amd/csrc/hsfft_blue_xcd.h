@@ -74,6 +74,7 @@ struct XArgs {
     unsigned *err;        /* sticky error word */
     unsigned batch, ng, nsig, sleep;
     unsigned jitter;      /* > 0: pseudo-random per-phase delays (uneven-load tests; results unchanged) */
+    unsigned merge;       /* 1: one acquire per iteration when both counters are already complete */
     unsigned xmap;        /* 1: a group spans the XCDs (XCD x owns tiles [8x, 8x+8) of every group) */
     unsigned *dbg;        /* optional per-workgroup trace (8 words): rows, P1, wait A, P2, wait B, P3 */
 };
@@ -119,31 +120,37 @@ __device__ __forceinline__ void arrive(const XArgs &a, unsigned *c, unsigned k, 
     if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* wait until the group's counter reaches `target` (R1 consumer: one lane polls relaxed, then
+/* wait until the group's counter c reaches `target` (R1 consumer: one lane polls relaxed, then
  * ONE agent-scope acquire and its vmcnt(0), then the barrier every wave joins before loading);
- * false on timeout (~1.3 s without progress of this one wait) or sticky error */
+ * false on timeout (~1.3 s without progress of this one wait) or sticky error.  If c2 is given
+ * and has already reached target2 when c is satisfied, the same acquire covers it too and
+ * *both is set (the caller then skips its wait on c2: one acquire per iteration instead of
+ * two). */
 __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned target, unsigned *sflag, unsigned k,
-                                      unsigned ph)
+                                      unsigned ph, unsigned *c2 = nullptr, unsigned target2 = 0, bool *both = nullptr)
 {
     if (threadIdx.x == 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); /* deadline per wait */
-        unsigned bad = 0;
+        unsigned st = 0;
         while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             for (unsigned n = 0; n < a.sleep; n++) __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > T_LIMIT ||
                 __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                bad = 1;
+                st = 1;
                 break;
             }
         }
+        if (!st && c2 && __hip_atomic_load(c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target2) st = 2;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); /* buffer_inv sc1: drop this CU's stale L1 lines */
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the invalidate has completed */
-        *sflag = bad;
+        *sflag = st;
     }
     jitter_sleep(a, k, ph + 8);
     __syncthreads();
-    return __builtin_amdgcn_readfirstlane(*sflag) == 0;
+    const unsigned st = __builtin_amdgcn_readfirstlane(*sflag);
+    if (both) *both = st == 2;
+    return (st & 1) == 0;
 }
 
 template <int S>
@@ -213,8 +220,10 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
     }
         double xr[8], xi[8];
         double2 w[7];
+        bool a_ready = false; /* A(k) observed complete before P3's acquire: P2 needs no wait */
         if (k >= 2) { /* ---- P3 of row k-2: k_blast's body on image 2 [k&1], chirp store */
-            if (!await(a, cB, (k - 1) * NTILE, sflag, k, 0)) return;
+            if (!await(a, cB, (k - 1) * NTILE, sflag, k, 0, a.merge && k <= R ? cA : nullptr, k * NTILE, &a_ready))
+                return;
             BX_MARK(4)
             /* per-thread indices from an opaque copy of threadIdx in every phase, so the
              * compiler does not hoist all three phases' addresses out of the loop (spills) */
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
             tr[0]++;
         }
         if (k >= 1 && k <= R) { /* ---- P2 of row k-1: k_bmid's body, image 1 -> image 2 [(k-1)&1] */
-            if (!await(a, cA, k * NTILE, sflag, k, 1)) return;
+            if (!a_ready && !await(a, cA, k * NTILE, sflag, k, 1)) return;
             BX_MARK(2)
             unsigned tt = tid;
             asm volatile("" : "+v"(tt));

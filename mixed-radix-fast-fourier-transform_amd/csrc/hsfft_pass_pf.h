@@ -502,8 +502,9 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *ltw = lds + P * G, *cry = ltw + 504;
     double *ld = reinterpret_cast<double *>(lds); /* [0, 4096): split image / hi imag, [4096, 8192): hi real */
-    /* a.tile_major: consecutive blocks (one XCD) take the same walk segment of consecutive rows,
-     * so the segment's twiddle runs and twiddle2 slice are read from that XCD's L2 */
+    /* a.tile_major (1, 2): consecutive blocks (one XCD) take the same walk segment of
+     * consecutive rows, so the segment's twiddle runs and twiddle2 slice are read from that
+     * XCD's L2 */
     const unsigned blk = xcd_remap(blockIdx.x), nb = (unsigned)a.batch;
     const unsigned b = a.tile_major ? blk % nb : blk / (W + 1), s = a.tile_major ? blk / nb : blk % (W + 1);
     const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
@@ -538,14 +539,20 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
         }
         return;
     }
-    const unsigned j0 = s * T, j1 = min(j0 + T, B / 16);
+    const unsigned j0 = s * T, j1 = min(j0 + T, B / 16), len = j1 - j0;
+    /* a.tile_major == 2: the walk starts at tile o of its segment and wraps (two chains:
+     * [j0+o, j1) then [j0, j0+o)), o from the row, so the workgroups of one XCD that share a
+     * segment (and its twiddles, from L2) read and write at different offsets of their rows --
+     * rows lie 32 MiB apart, so equal offsets would land in the same DRAM channels */
+    const unsigned o = a.tile_major == 2 && len > 0 ? (b * 7u) % len : 0u;
     R2cBuf A, Bf;
-    r2cw2_issue(A, row, B, B - 8 * j0 - 8, a.tw, tid0); /* hi(j0) */
+    r2cw2_issue(A, row, B, B - 8 * (j0 + o) - 8, a.tw, tid0); /* hi of the first tile */
 #pragma unroll 1
-    for (unsigned j = j0; j < j1; j++) {
+    for (unsigned jr = 0; jr < len; jr++) {
         unsigned tid = tid0;
         asm volatile("" : "+v"(tid));
         const unsigned g = tid & 7, jt = tid >> 3;
+        const unsigned j = j0 + (o + jr) % len;
         const unsigned qlo = 8 * j + 1;
         r2cw2_issue(Bf, row, B, qlo, a.tw, tid); /* lo(j) loads while hi(j) is transformed */
         double2 w2[7];
@@ -559,8 +566,9 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
         r2cw2_tw(Bf, w2, lds, ltw, tid);
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) ld[4096 + (jt + jj * TPG) * G + g] = A.r[jj]; /* hi real parts wait here */
-        {   /* hi(j+1) loads while lo(j) is transformed; unconditional (the last tile reloads) */
-            const unsigned jn = j + 1 < j1 ? j + 1 : j;
+        {   /* the next tile's hi loads while lo(j) is transformed; unconditional (the last tile
+             * reloads itself) */
+            const unsigned jn = jr + 1 < len ? j0 + (o + jr + 1) % len : j;
             r2cw2_issue(A, row, B, B - 8 * jn - 8, a.tw, tid);
         }
         r2c_stages<SGN, true>(Bf.r, Bf.i, w2, lds, ltw, tid);
@@ -569,7 +577,7 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
         for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
         __syncthreads();
         /* ---- pairs: X[N-k], X[h-k] aligned; X[k], X[h+k] shifted one lane onto line [8j, 8j+8) */
-        const bool first = j == j0;
+        const bool cstart = jr == 0 || j == j0; /* a chain starts: no carry for this line */
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
             const unsigned u = jt + jj * TPG, k = u * B + qlo + g, hk = h - k;
@@ -586,22 +594,26 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
                 X[p] = va;
                 X[h + p] = vb;
             } else {
-                if (!first) {
+                if (!cstart) {
                     X[p] = cry[u];
                     X[h + p] = cry[512 + u];
+                } else if (jr != 0 && j1 < B / 16) { /* the first chain's carry: bin 8*j1 */
+                    X[u * B + 8 * j1] = cry[u];
+                    X[h + u * B + 8 * j1] = cry[512 + u];
                 }
                 cry[u] = va;
                 cry[512 + u] = vb;
             }
         }
     }
-    /* the last tile's carries (bin 8*j1 of X[k] / X[h+k]; at the row's last tile column B/2,
-     * already written by the aligned streams) */
-    if (j1 < B / 16 && j1 > j0 && (tid0 & 7) == 0) {
+    /* the last chain's carry: bin 8*(j0+o), or 8*j1 without rotation (at the row's last tile,
+     * column B/2, already written by the aligned streams) */
+    const unsigned jend = o > 0 ? j0 + o : j1;
+    if (len > 0 && jend < B / 16 && (tid0 & 7) == 0) {
         const unsigned jt = tid0 >> 3;
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
-            const unsigned u = jt + jj * TPG, p = u * B + 8 * j1;
+            const unsigned u = jt + jj * TPG, p = u * B + 8 * jend;
             X[p] = cry[u];
             X[h + p] = cry[512 + u];
         }
@@ -634,7 +646,9 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
         void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk2<1> : k_r2c_walk2<-1>;
-        a.tile_major = env("HSFFT_R2C_ORDER", 0); /* measured 87-93 vs 101: the rows' DRAM pages matter more */
+        /* HSFFT_R2C_ORDER 1: segment-major (measured 88.7-90.8 vs 95.4-101.4 row-major), 2: the
+         * same with the walk start rotated per row */
+        a.tile_major = env("HSFFT_R2C_ORDER", 0);
         HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW2_LDS));
         hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), R2CW2_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());

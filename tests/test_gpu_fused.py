@@ -134,16 +134,18 @@ def test_bluestein_row_looped_kernels(n, mask, xt, monkeypatch):
 
 
 @pytest.mark.parametrize("ng,batch,jitter", [("8", 1, "0"), ("8", 5, "0"), ("8", 19, "0"), ("3", 7, "0"), ("1", 2, "0"),
-                                             ("8", 19, "3"), ("3", 7, "5")])
+                                             ("8", 19, "3"), ("3", 7, "5"), ("8", 19, "m0"), ("8", 19, "m0j3")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
 def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
     """Bluestein M = 2^18 as one persistent launch (csrc/hsfft_blue_xcd.h: groups of 64
     workgroups carry a row through the three passes, intermediates handed over in-launch):
     fewer rows than groups, ragged last round, both signs, and under uneven load (HSFFT_BX_JITTER:
     pseudo-random per-phase delays scramble the hand-off order) -- bit-exact vs the oracle and
-    vs the three-launch path; no launch fell back."""
+    vs the three-launch path; no launch fell back.  m0: one acquire per wait instead of the
+    merged acquire per iteration (HSFFT_BX_MERGE=0)."""
     monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
-    monkeypatch.setenv("HSFFT_BX_JITTER", jitter)
+    monkeypatch.setenv("HSFFT_BX_MERGE", "0" if jitter.startswith("m0") else "1")
+    monkeypatch.setenv("HSFFT_BX_JITTER", jitter[3:] if jitter.startswith("m0j") else ("0" if jitter == "m0" else jitter))
     fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
     x = T.complex_input(n, 0xB7 ^ n ^ batch, batch=batch).reshape(batch, n)
     for sgn in (1, -1):
