@@ -74,6 +74,23 @@ __device__ __forceinline__ void b_tile(double2 *row, unsigned q0)
     for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, ((jt + 64 * i) * QB + q0 + g) * 16u, 0, 0);
 }
 
+template <bool SC1>
+__device__ __forceinline__ void b_load(const double2 *row, unsigned q0, u4 (&v)[8])
+{
+    const unsigned g = threadIdx.x & 7, jt = threadIdx.x >> 3;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)row, 0, (int)(N * 16u), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((jt + 64 * i) * QB + q0 + g) * 16u, 0, SC1 ? 16 : 0);
+}
+
+__device__ __forceinline__ void b_store(double2 *row, unsigned q0, const u4 (&v)[8])
+{
+    const unsigned g = threadIdx.x & 7, jt = threadIdx.x >> 3;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, (int)(N * 16u), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, ((jt + 64 * i) * QB + q0 + g) * 16u, 0, 0);
+}
+
 /* two-launch replica: pass A (grid = rows x 128 items), pass B (rows x 256 tiles) */
 __global__ __launch_bounds__(512) void k_pass_a(const double2 *in, double2 *out)
 {
@@ -91,8 +108,30 @@ struct OArgs {
     const double2 *in;
     double2 *out;
     unsigned *adone, *bdone, *err;
-    unsigned rows, na, nb, lag;
+    unsigned rows, na, nb, lag, pref;
 };
+
+/* B poller: wait until row `row` has all its pass-A items, then one agent acquire; false on
+ * timeout */
+__device__ __forceinline__ bool b_wait(const OArgs &a, unsigned row, unsigned long long t0, unsigned *flag)
+{
+    if (threadIdx.x == 0) {
+        unsigned bad = 0;
+        while (__hip_atomic_load(&a.adone[row * CS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ITEMS) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > T_LIMIT) {
+                __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bad = 1;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *flag = bad;
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(*flag) == 0;
+}
 
 /* one-launch replica (fixed roles): A workgroups take items it = a, a + na, ... in row order
  * and stay at most `lag` rows ahead of the pass-B tiles; B workgroups own tiles b, b + nb, ...
@@ -122,23 +161,35 @@ __global__ __launch_bounds__(512) void k_one(OArgs a)
     }
     const unsigned b = blockIdx.x - a.na;
     for (unsigned tile = b; tile < TILES; tile += a.nb) {
-        for (unsigned row = 0; row < a.rows; row++) {
-            if (threadIdx.x == 0) {
-                unsigned bad = 0;
-                while (__hip_atomic_load(&a.adone[row * CS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ITEMS) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > T_LIMIT) {
-                        __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        bad = 1;
-                        break;
-                    }
+        if (a.pref) { /* the next row's tile loads while this row's tile is stored */
+            u4 v0[8], v1[8];
+            if (!b_wait(a, 0, t0, &flag)) return;
+            b_load<true>(a.out, tile * 8, v0);
+            for (unsigned row = 0; row < a.rows; row += 2) {
+                const bool more = row + 1 < a.rows;
+                if (more) {
+                    if (!b_wait(a, row + 1, t0, &flag)) return;
+                    b_load<true>(a.out + (size_t)(row + 1) * N, tile * 8, v1);
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                b_store(a.out + (size_t)row * N, tile * 8, v0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                flag = bad;
+                __syncthreads();
+                if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.bdone[row * CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!more) break;
+                const bool more2 = row + 2 < a.rows;
+                if (more2) {
+                    if (!b_wait(a, row + 2, t0, &flag)) return;
+                    b_load<true>(a.out + (size_t)(row + 2) * N, tile * 8, v0);
+                }
+                b_store(a.out + (size_t)(row + 1) * N, tile * 8, v1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.bdone[(row + 1) * CS], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            __syncthreads();
-            if (__builtin_amdgcn_readfirstlane(flag)) return;
+            continue;
+        }
+        for (unsigned row = 0; row < a.rows; row++) {
+            if (!b_wait(a, row, t0, &flag)) return;
             b_tile<true>(a.out + (size_t)row * N, tile * 8);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -172,7 +223,7 @@ struct Ctx {
     double2 *in, *out;
     unsigned *ctr, *err;
     size_t ctr_bytes;
-    unsigned rows, na, nb, lag;
+    unsigned rows, na, nb, lag, pref;
 };
 
 int main(int argc, char **argv)
@@ -212,12 +263,13 @@ int main(int argc, char **argv)
     report("two-launch replica: pass A movement", ta);
     report("two-launch replica: pass B movement", tb);
     report("two-launch replica: A + B", ta + tb);
-    const unsigned cfg[][3] = {{256, 256, 2}, {256, 256, 4}, {256, 256, 8}, {256, 256, 16}, {256, 256, 64},
-                               {128, 384, 4}, {384, 128, 4}, {256, 256, 100000}};
+    const unsigned cfg[][4] = {{256, 256, 8, 0}, {256, 256, 100000, 0}, {128, 384, 4, 0}, {256, 256, 4, 1}, {256, 256, 8, 1},
+                               {256, 256, 16, 1}, {256, 256, 100000, 1}, {128, 384, 8, 1}, {192, 320, 8, 1}};
     for (auto &g : cfg) {
         c.na = g[0];
         c.nb = g[1];
         c.lag = g[2];
+        c.pref = g[3];
         float t = timed(e0, e1, [](void *p) {
             Ctx *c = (Ctx *)p;
             CK(hipMemsetAsync(c->ctr, 0, c->ctr_bytes, 0));
@@ -231,13 +283,14 @@ int main(int argc, char **argv)
             a.na = c->na;
             a.nb = c->nb;
             a.lag = c->lag;
+            a.pref = c->pref;
             hipLaunchKernelGGL(k_one, dim3(c->na + c->nb), dim3(512), 0, 0, a);
         }, &c, 3);
         unsigned err = 0;
         CK(hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
         char name[96];
-        snprintf(name, sizeof name, "one-launch replica: %u A + %u B workgroups, lag %u rows%s", g[0], g[1], g[2],
-                 err ? " [WAIT TIMED OUT]" : "");
+        snprintf(name, sizeof name, "one-launch replica: %u A + %u B wgs, lag %u rows%s%s", g[0], g[1], g[2],
+                 g[3] ? ", B prefetch" : "", err ? " [WAIT TIMED OUT]" : "");
         report(name, t);
     }
     return 0;
