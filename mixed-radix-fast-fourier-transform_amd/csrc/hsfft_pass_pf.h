@@ -639,16 +639,16 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     a.B = B;
     a.batch = batch;
     a.tiles = a.tiles_q = B / 16 + 1;
-    /* default: k_r2c_walk2, 32 tile pairs per walk (c5 98.4 -> 100.6-101.4 GSamples/s);
-     * HSFFT_R2C_WALK=0 (and the compact layout): k_r2c_fused */
+    /* default: k_r2c_walk2, walks of 16 tile pairs, segment-major with the walk start rotated
+     * per row (HSFFT_R2C_ORDER=2): c5 98.9 vs 93.0-93.8 GSamples/s row-major with 32-pair walks
+     * on one box (order 2 with walks of 8 / 32: 95.0 / 95.7; plain segment-major (1) 88.7-90.8
+     * on another); HSFFT_R2C_WALK=0 (and the compact layout): k_r2c_fused */
     if (!compact && env("HSFFT_R2C_WALK", 2) != 0) {
-        const long long T = env("HSFFT_R2C_WT", 32) > 0 ? env("HSFFT_R2C_WT", 32) : 32, W = (B / 16 + T - 1) / T;
+        const long long T = env("HSFFT_R2C_WT", 16) > 0 ? env("HSFFT_R2C_WT", 16) : 16, W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
         void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk2<1> : k_r2c_walk2<-1>;
-        /* HSFFT_R2C_ORDER 1: segment-major (measured 88.7-90.8 vs 95.4-101.4 row-major), 2: the
-         * same with the walk start rotated per row */
-        a.tile_major = env("HSFFT_R2C_ORDER", 0);
+        a.tile_major = env("HSFFT_R2C_ORDER", 2); /* 0 row-major, 1 segment-major, 2 rotated */
         HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW2_LDS));
         hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), R2CW2_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());
