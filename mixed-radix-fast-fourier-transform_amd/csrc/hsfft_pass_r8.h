@@ -122,15 +122,55 @@ __device__ __forceinline__ void do_stage(double (&xr)[8], double (&xi)[8], const
 
 /* stage s outputs -> LDS -> stage s+1 inputs.  SPLIT exchanges the real parts, then the
  * imaginary parts, through a P*G-double image (half the LDS, so twice the workgroups per CU). */
-/* LDS slot of point p.  After a leaf stage (LLOC == 1) consecutive butterflies write R
- * points apart; with fewer than 8 groups per 128-B bank window that is an R-way bank
- * conflict, so the low bits are XOR-swizzled with the butterfly index (conflict-free
- * writes, and the reads of the next stage stay contiguous). */
-template <int R, int LLOC, int G>
+/* LDS slot of point p: an XOR swizzle of p's low bits with higher bits (a bijection on
+ * [0, P), applied by the writes and the reads of the same exchange), chosen per exchange shape
+ * so that the wave's stores hit distinct banks.
+ *  - 16-B exchanges (double2 per point): after a leaf stage (LLOC == 1) consecutive butterflies
+ *    write R points apart; with fewer than 8 groups per 128-B bank window that is an R-way
+ *    conflict, so p ^= (p / R) & (R - 1).
+ *  - split exchanges (8-B doubles, real then imaginary parts), after a leaf stage only:
+ *    p ^= (p >> s) & (R - 1) with s per (R, G), found with a bank model of ds_write_b64 (4
+ *    groups of 16 lanes, 32 banks) and ds_read_b64 (2 groups of 32 lanes, 64 banks): the first
+ *    exchange of the [4,8,8,8] first pass (G = 2, c2's pass A) goes from 8 to 4 cycles per store
+ *    instruction (conflict-free), that of [8,8,8,8] (G = 1, c5's pass A) from 8 to 4; the reads
+ *    stay conflict-free (round 2's swizzle: s = log2 R). */
+struct Swz {
+    int t, k, s;
+};
+
+constexpr int swz_log2(int x) { return x <= 1 ? 0 : 1 + swz_log2(x / 2); }
+
+constexpr Swz split_swz(int R, int LLOC, int G)
+{
+    /* write groups of 16 lanes cover 16 / G butterflies; their R outputs jj sit LLOC apart */
+    const int lg = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : -1;
+    if (lg < 0 || R < 2) return {0, 0, 0};
+    if (LLOC == 1) { /* XOR the jj bits with the butterfly index bits above the bank window */
+        const int k = swz_log2(R);
+        return {0, k, (4 - lg) > k ? 4 - lg : k};
+    }
+    /* later exchanges (LLOC > 1) keep the identity: a swizzle there has to XOR the jj bits of
+     * the write address with the butterfly's ml bits, which turns the eight constant store
+     * offsets into per-jj address arithmetic -- the bank model says the [4,8,8,8] / [8,8,8,8]
+     * second exchanges would go from 8 to 4 cycles per store, but hipcc then spills 4-7 dwords
+     * in pf::k_firstq (measured in the code object), so it is not used */
+    return {0, 0, 0};
+}
+
+template <int R, int LLOC, int G, bool SPLIT = false>
 __device__ __forceinline__ unsigned lds_slot(unsigned p)
 {
-    if constexpr (LLOC == 1 && G < 8 && R > 1) return p ^ ((p / R) & (R - 1));
-    return p;
+#ifndef HSFFT_SPLIT_SWZ_R2 /* (experiment builds: -DHSFFT_SPLIT_SWZ_R2 keeps round 2's swizzle) */
+    if constexpr (SPLIT) {
+        constexpr Swz z = split_swz(R, LLOC, G);
+        if constexpr (z.k > 0) return p ^ (((p >> z.s) & ((1u << z.k) - 1u)) << z.t);
+        return p;
+    } else
+#endif
+    {
+        if constexpr (LLOC == 1 && G < 8 && R > 1) return p ^ ((p / R) & (R - 1));
+        return p;
+    }
 }
 
 /* Materialise LDS-loaded values before the barrier that follows their loads.  Without it
@@ -186,7 +226,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
                 const unsigned b = c * TPG + jt;
                 const unsigned kloc = b & (LLOC - 1), ml = b / LLOC;
 #pragma unroll
-                for (int jj = 0; jj < R; jj++) ld[lds_slot<R, LLOC, G>(ml * LLOC * R + kloc + jj * LLOC) * G + g] = x[c * R + jj];
+                for (int jj = 0; jj < R; jj++) ld[lds_slot<R, LLOC, G, true>(ml * LLOC * R + kloc + jj * LLOC) * G + g] = x[c * R + jj];
             }
             __syncthreads();
 #pragma unroll
@@ -194,7 +234,7 @@ __device__ __forceinline__ void exchange(double (&xr)[8], double (&xi)[8], doubl
                 const unsigned b = c * TPG + jt;
                 const unsigned kloc = b & (L2 - 1), ml = b / L2;
 #pragma unroll
-                for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[lds_slot<R, LLOC, G>((ml + i * S2) * L2 + kloc) * G + g];
+                for (int i = 0; i < R2; i++) x[c * R2 + i] = ld[lds_slot<R, LLOC, G, true>((ml + i * S2) * L2 + kloc) * G + g];
             }
             pin(x);
             __syncthreads();
