@@ -67,20 +67,25 @@ static conv_pair conv_plans(int P)
         if (g_cache[k].refs == 0 && (victim < 0 || !g_cache[k].f || (g_cache[victim].f && g_cache[k].used < g_cache[victim].used)))
             victim = k;
     }
-    if (victim >= 0) { /* evict the least recently used idle slot */
-        if (g_cache[victim].f) {
-            free_real_fft(g_cache[victim].f);
-            free_real_fft(g_cache[victim].i);
-        }
+    if (victim >= 0) { /* reserve the least recently used idle slot; build and free outside
+                        * the lock (plans of other lengths / devices are not held up) */
+        fft_real_object of = g_cache[victim].f, oi = g_cache[victim].i;
         g_cache[victim].P = P;
         g_cache[victim].mode = mode;
         g_cache[victim].refs = 1;
         g_cache[victim].used = ++g_cache_clock;
-        g_cache[victim].f = fft_real_init(P, 1);
-        g_cache[victim].i = fft_real_init(P, -1);
-        cp.f = g_cache[victim].f;
-        cp.i = g_cache[victim].i;
+        g_cache[victim].f = g_cache[victim].i = NULL; /* building: no other thread matches it */
+        pthread_mutex_unlock(&g_clock);
+        if (of) {
+            free_real_fft(of);
+            free_real_fft(oi);
+        }
+        cp.f = fft_real_init(P, 1);
+        cp.i = fft_real_init(P, -1);
         cp.slot = victim;
+        pthread_mutex_lock(&g_clock);
+        g_cache[victim].f = cp.f;
+        g_cache[victim].i = cp.i;
         pthread_mutex_unlock(&g_clock);
         return cp;
     }
