@@ -293,6 +293,36 @@ def c1_latency(iters=300, warmup=20):
     return lat
 
 
+def c1_threads(nthreads=8, iters=200):
+    """N=1024 fft_exec on host buffers from `nthreads` host threads at once, one plan shared
+    (the reference's fft_exec is reentrant): mean wall time per transform over all threads"""
+    import threading
+    import numpy as np
+    L = hsfft.lib()
+    p1 = hsfft.Plan(1024, 1)
+    xs = [np.ascontiguousarray(np.exp(1j * (np.arange(1024.0) + t))) for t in range(nthreads)]
+    ys = [np.zeros_like(x) for x in xs]
+
+    def work(t, k):
+        px, py = xs[t].ctypes.data_as(ctypes.c_void_p), ys[t].ctypes.data_as(ctypes.c_void_p)
+        for _ in range(k):
+            L.fft_exec(p1.ptr, px, py)
+    ths = [threading.Thread(target=work, args=(t, 20)) for t in range(nthreads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    ths = [threading.Thread(target=work, args=(t, iters)) for t in range(nthreads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - t0
+    p1.close()
+    return wall / (nthreads * iters) * 1e6
+
+
 def c1_cpu_baseline(seed=0x5EED0001, reps=200000):
     """the reference's fft_exec for N=1024 on ONE host core (its own single-thread design)"""
     ref_so = os.path.join(REPO, "oracle", "_ref", "libhsref.so")
@@ -318,7 +348,8 @@ def other_configs(steps=10, warmup=2, cpu=True, cpu_seconds=8.0):
     lat = c1_latency()
     out["c1"] = {"value": round(lat[len(lat) // 2] * 1e6, 2), "unit": "us", "workload": CONFIGS["c1"][4],
                  "higher_is_better": False, "steps": len(lat),
-                 "latency_us": {"p10": round(lat[len(lat) // 10] * 1e6, 2), "p90": round(lat[len(lat) * 9 // 10] * 1e6, 2)}}
+                 "latency_us": {"p10": round(lat[len(lat) // 10] * 1e6, 2), "p90": round(lat[len(lat) * 9 // 10] * 1e6, 2)},
+                 "threads8_us_per_transform": round(c1_threads(), 2)}
     if cpu:
         out["c1"]["cpu_baseline"] = c1_cpu_baseline()
     L = hsfft.lib()

@@ -62,7 +62,8 @@ int set_err(hipError_t e, const char *what)
 
 hipStream_t g_stream2[HS_MAX_DEV], g_stream3[HS_MAX_DEV];
 std::atomic<bool> g_stream2_init[HS_MAX_DEV], g_stream3_init[HS_MAX_DEV];
-thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream */
+thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream, 3: this thread's own */
+thread_local hipStream_t t_own[HS_MAX_DEV]; /* per-thread streams (concurrent small fft_exec calls) */
 
 int cur_dev()
 {
@@ -79,6 +80,10 @@ hipStream_t stream()
 {
     if (t_sidx == 0) return primary();
     const int dev = cur_dev();
+    if (t_sidx == 3) {
+        if (!t_own[dev] && hipStreamCreateWithFlags(&t_own[dev], hipStreamNonBlocking) != hipSuccess) t_own[dev] = 0;
+        return t_own[dev];
+    }
     if (t_sidx == 2) return lazy_stream(g_stream3, g_stream3_init, dev);
     return lazy_stream(g_stream2, g_stream2_init, dev);
 }
@@ -778,7 +783,7 @@ int hsd_cu_count(void)
 
 int hsd_select_stream(int idx)
 {
-    t_sidx = idx < 0 || idx > 2 ? 0 : idx;
+    t_sidx = idx < 0 || idx > 3 ? 0 : idx;
     return 0;
 }
 

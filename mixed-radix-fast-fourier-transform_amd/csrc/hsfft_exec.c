@@ -951,8 +951,64 @@ static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
     if (rc) fatal("fft_exec failed");
 }
 
+/* Small host-buffer transforms without the device lock: one-pass mixed-radix plans on host
+ * buffers run on this thread's own stream with this thread's own page-locked slots, so
+ * threads calling fft_exec at once overlap their launches, transfers and waits instead of
+ * taking turns on the device lock (the reference's fft_exec is reentrant on a shared plan,
+ * highSpeedFFT.c:1920-1942).  The device lock is held only while the plan's device state is
+ * built.  Returns 1 when the call does not qualify (then the locked path runs). */
+static __thread void *t_pin[HS_MAX_DEV][2];
+static __thread size_t t_pin_sz[HS_MAX_DEV];
+
+static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *oup)
+{
+    if (obj == NULL || inp == NULL || oup == NULL || (obj->lt != 0 && obj->lt != 1)) return 1; /* locked path reports */
+    if (obj->lt != 0 || !env_int("HSFFT_SMALL_CONCURRENT", 1)) return 1;
+    g_errbuf[0] = 0;
+    if (hs_require_gpu()) return 1;
+    const size_t bytes = sizeof(fft_data) * (size_t)obj->N;
+    if (bytes > (size_t)env_int("HSFFT_SMALL_KB", 1024) * 1024) return 1;
+    const int d = hsd_get_device();
+    if (d < 0 || d >= HS_MAX_DEV || hsd_is_device_ptr(inp) || hsd_is_device_ptr(oup)) return 1;
+    hs_entry *e = hs_entry_get(obj);
+    if (!e) return 1;
+    if (e->lt != 0 || e->npass != 1) {
+        hs_entry_put(e);
+        return 1;
+    }
+    hs_lock_device(); /* the plan's device state is built once, under the lock */
+    hs_devstate *ds = devstate(e);
+    hs_unlock_device(d);
+    if (!ds) {
+        hs_entry_put(e);
+        return 1;
+    }
+    if (t_pin_sz[d] < bytes) {
+        hsd_host_free(t_pin[d][0]);
+        hsd_host_free(t_pin[d][1]);
+        t_pin[d][0] = hsd_host_alloc(bytes);
+        t_pin[d][1] = hsd_host_alloc(bytes);
+        t_pin_sz[d] = t_pin[d][0] && t_pin[d][1] ? bytes : 0;
+        if (!t_pin_sz[d]) {
+            hs_entry_put(e);
+            return 1;
+        }
+    }
+    memcpy(t_pin[d][0], inp, bytes);
+    hsd_select_stream(3);
+    int rc = run_chain(e, ds, t_pin[d][0], obj->N, t_pin[d][1], obj->N, 1, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL,
+                       HS_STORE_PLAIN, NULL, e->M);
+    if (!rc) rc = hsd_stream_sync();
+    hsd_select_stream(0);
+    hs_entry_put(e);
+    if (rc) fatal("fft_exec failed");
+    memcpy(oup, t_pin[d][1], bytes);
+    return 0;
+}
+
 void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
 {
+    if (small_host_exec_concurrent(obj, inp, oup) == 0) return;
     const int d = hs_lock_device();
     fft_exec_locked(obj, inp, oup);
     hs_unlock_device(d);

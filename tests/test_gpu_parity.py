@@ -154,12 +154,16 @@ def test_c2c_exact_twiddle_mode_every_length_2_to_8192():
     assert not bad, bad[:20]
 
 
-def test_c2c_dropin_every_length_2_to_4096():
+@pytest.mark.parametrize("concurrent", ["1", "0"])
+def test_c2c_dropin_every_length_2_to_4096(concurrent, monkeypatch):
     """the drop-in fft_exec on host buffers (one-pass plans take the page-locked zero-copy
-    path, the others the staged path) for every length 2..4096, alternating signs, bit-exact
-    vs the oracle (highSpeedFFT.c:1920-1942 fft_exec)."""
+    path -- on this thread's own stream without the device lock by default, under the device
+    lock on the library stream with HSFFT_SMALL_CONCURRENT=0 -- the others the staged path)
+    for every length 2..4096 (every 7th with the locked path), alternating signs, bit-exact vs
+    the oracle (highSpeedFFT.c:1920-1942 fft_exec)."""
+    monkeypatch.setenv("HSFFT_SMALL_CONCURRENT", concurrent)
     bad = []
-    for n in range(2, 4097):
+    for n in range(2, 4097, 1 if concurrent == "1" else 7):
         sgn = 1 if n % 2 else -1
         x = T.complex_input(n, T.seed_for(n) ^ 0x6161)
         p = hsfft.Plan(n, sgn)
