@@ -544,7 +544,12 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
      * [j0+o, j1) then [j0, j0+o)), o from the row, so the workgroups of one XCD that share a
      * segment (and its twiddles, from L2) read and write at different offsets of their rows --
      * rows lie 32 MiB apart, so equal offsets would land in the same DRAM channels */
-    const unsigned o = a.tile_major == 2 && len > 0 ? (b * 7u) % len : 0u;
+    /* tile_major >= 3: only tile_major - 1 rotation classes, evenly spaced, so groups of
+     * workgroups share a tile (and its twiddles) at the same time */
+    const unsigned nrot = a.tile_major >= 3 ? (unsigned)a.tile_major - 1 : 0u;
+    const unsigned o = len == 0 ? 0u
+                     : a.tile_major == 2 ? (b * 7u) % len
+                     : nrot ? ((b % nrot) * len) / nrot : 0u;
     R2cBuf A, Bf;
     r2cw2_issue(A, row, B, B - 8 * (j0 + o) - 8, a.tw, tid0); /* hi of the first tile */
 #pragma unroll 1

@@ -589,7 +589,8 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wt", ["walk0", "w2:16", "w2:1", "w2:5", "w2:4096", "o1:8", "o2:8", "o2:5", "o2:32", "o2:4096"])
+@pytest.mark.parametrize("wt", ["walk0", "w2:16", "w2:1", "w2:5", "w2:4096", "o1:8", "o2:8", "o2:5", "o2:32", "o2:4096",
+                                "o3:16", "o5:16", "o5:5", "o9:8"])
 @pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
 def test_r2c_walk(n, sgn, wt, monkeypatch):
     """pf::k_r2c_walk2 (default split kernel of the reference-layout r2c): walks of WT tile
@@ -597,7 +598,8 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
     tile is a walk's first (partial first line, carry written at once); 5: walks of uneven
     length and a short last walk; 4096: one walk per row (the carry reaches column B/2);
     walk0: the one-tile-per-workgroup k_r2c_fused; o1 / o2: segment-major block order, o2 with
-    the walk start rotated per row (two carry chains per walk).  Bit-exact vs the oracle, odd
+    the walk start rotated per row (two carry chains per walk), o3 / o5 / o9 with 2 / 4 / 8
+    evenly spaced rotation classes.  Bit-exact vs the oracle, odd
     batch, stale output buffer."""
     if wt == "walk0":
         monkeypatch.setenv("HSFFT_R2C_WALK", "0")
