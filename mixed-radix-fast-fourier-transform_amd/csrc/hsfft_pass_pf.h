@@ -644,16 +644,20 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
     a.B = B;
     a.batch = batch;
     a.tiles = a.tiles_q = B / 16 + 1;
-    /* default: k_r2c_walk2, walks of 16 tile pairs, segment-major with the walk start rotated
-     * per row (HSFFT_R2C_ORDER=2): c5 98.9 vs 93.0-93.8 GSamples/s row-major with 32-pair walks
-     * on one box (order 2 with walks of 8 / 32: 95.0 / 95.7; plain segment-major (1) 88.7-90.8
-     * on another); HSFFT_R2C_WALK=0 (and the compact layout): k_r2c_fused */
+    /* default: k_r2c_walk2, walks of 8 tile pairs, segment-major, the walk start of row b at
+     * tile b % 8 (HSFFT_R2C_ORDER=9: 8 rotation classes).  Interleaved on one box (two passes
+     * each, GSamples/s): 105.8 / 105.8 vs 103.5-104.3 for the (b*7) % 16 rotation with walks of
+     * 16 (ORDER=2), 99.7-99.8 row-major with walks of 32 (0), 98.4-98.8 with 4 classes and 94.3-94.7
+     * with 2 (ORDER=5, 3: FETCH 32.3 / 29.3 GB per 512 rows, the twiddles mostly from L2, yet
+     * slower: workgroups that read the same lines at the same time contend); plain
+     * segment-major (1) 88.7-90.8 elsewhere; HSFFT_R2C_WALK=0 (and the compact layout):
+     * k_r2c_fused */
     if (!compact && env("HSFFT_R2C_WALK", 2) != 0) {
-        const long long T = env("HSFFT_R2C_WT", 16) > 0 ? env("HSFFT_R2C_WT", 16) : 16, W = (B / 16 + T - 1) / T;
+        const long long T = env("HSFFT_R2C_WT", 8) > 0 ? env("HSFFT_R2C_WT", 8) : 8, W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
         void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk2<1> : k_r2c_walk2<-1>;
-        a.tile_major = env("HSFFT_R2C_ORDER", 2); /* 0 row-major, 1 segment-major, 2 rotated */
+        a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
         HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW2_LDS));
         hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), R2CW2_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());
