@@ -1,0 +1,18 @@
+#!/bin/bash
+# round-3 GPU session J: full suite + the default bench line + kernel stats of the c5 default
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r3j.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_r3j.log
+case $rc in 0) ;; *) exit $rc;; esac
+timeout -k 10 600 python bench.py > gpurun_out/bench_default_r3j.log 2>&1 || exit $?
+grep '^{' gpurun_out/bench_default_r3j.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); r=d['roofline']
+    print('value', d['value'], 'ms', d['ms_per_step'], 'frac', r['frac'], 'pass_ms', r.get('pass_ms'), 'cpu', d['cpu_baseline']['value'], 'copy', d.get('stream_copy_gbs'))
+    for k,v in d.get('other_configs',{}).items(): print(' ', k, v.get('value'), v.get('unit'), v.get('frac'), (v.get('cpu_baseline') or {}).get('value'), v.get('threads8_us_per_transform'))
+"
+COUNTER_SETS="FETCH_SIZE|WRITE_SIZE" tools/profile.sh r03c5j --config c5 --steps 2 --warmup 1 || exit $?
+python3 tools/prof_summary.py gpurun_out/prof_r03c5j --json gpurun_out/prof_r03c5j/summary.json > gpurun_out/prof_r03c5j/summary.txt
+exit 0
