@@ -462,6 +462,9 @@ struct R2cBuf {
     double2 l;    /* this thread's entry of the stage-0/1 twiddle runs (threads < 504) */
 };
 
+/* TWP (timing probe, -DHSFFT_DEV_PROBES builds only): every tile reads column 0's twiddle
+ * runs (cache-resident; results wrong) */
+template <bool TWP = false>
 __device__ __forceinline__ void r2cw2_issue(R2cBuf &d, const double2 *row, unsigned B, unsigned q0, const double2 *tw,
                                             unsigned tid)
 {
@@ -473,12 +476,13 @@ __device__ __forceinline__ void r2cw2_issue(R2cBuf &d, const double2 *row, unsig
         d.r[i] = v.x;
         d.i[i] = v.y;
     }
+    const unsigned qt = TWP ? 0u : q0;
     r8::Args ta;
     ta.tw = tw;
     ta.B = B;
-    r8::load_tw_co<64>(d.w, ta, (int)(tid >> 3), q0);
+    r8::load_tw_co<64>(d.w, ta, (int)(tid >> 3), qt);
     const unsigned t = tid < 504 ? tid : 0, r = t / 56, e = t % 56;
-    const long long src = r == 0 ? (long long)B - 1 + 7LL * q0 + e : 8LL * B - 1 + 7LL * (q0 + (long long)B * (r - 1)) + e;
+    const long long src = r == 0 ? (long long)B - 1 + 7LL * qt + e : 8LL * B - 1 + 7LL * (qt + (long long)B * (r - 1)) + e;
     d.l = tw[src];
 }
 
@@ -495,9 +499,18 @@ __device__ __forceinline__ void r2cw2_tw(const R2cBuf &d, double2 (&w2)[7], doub
 
 constexpr int R2CW2_LDS = (512 * 8 + 504 + 1024) * 16;
 
-template <int SGN>
+/* V (measurement variants; 0 is the default): bit 0 phase trace into a.dbg; -DHSFFT_DEV_PROBES
+ * builds only (results WRONG): bit 1 twiddle2 read from one cache-resident line per lane group,
+ * bit 2 every tile's stage-2 twiddles from column 0.  Measured and dropped (round 3):
+ * non-temporal data loads and / or output stores (c5 88.3 / 91.3 / 85.2 vs 95.1-96.2 on one
+ * box); the lo tile's twiddle2 prefetched by LDS-DMA and the hi tile's into registers during
+ * the lo stages (bit-exact, 228 VGPRs: 104.6-105.0 vs 105.3-105.7 -- the wait moves from the
+ * pairs phase to the lo phase).  Probes: with no twiddle traffic at all c5 gains 2.5 %
+ * (108.3 / 107.7 vs 105.7 / 105.3): the twiddle re-reads are not what bounds the walk. */
+template <int SGN, int V = 0>
 __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsigned T, unsigned W)
 {
+    constexpr bool TRC = (V & 1) != 0, P_TW2 = (V & 2) != 0, P_TWS = (V & 4) != 0;
     constexpr int P = 512, TPG = 64, G = 8;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *ltw = lds + P * G, *cry = ltw + 504;
@@ -551,7 +564,16 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
                      : a.tile_major == 2 ? (b * 7u) % len
                      : nrot ? ((b % nrot) * len) / nrot : 0u;
     R2cBuf A, Bf;
-    r2cw2_issue(A, row, B, B - 8 * (j0 + o) - 8, a.tw, tid0); /* hi of the first tile */
+    /* phase trace (a.dbg): thread 0 sums 100 MHz ticks per phase -- [0] tile pairs, [1] hi
+     * twiddles + stages, [2] lo twiddles + stages, [3] pairs + stores */
+    unsigned tr1 = 0, tr2 = 0, tr3 = 0, tk = TRC ? (unsigned)__builtin_amdgcn_s_memrealtime() : 0u;
+#define R2C_MARK(acc)                                                         \
+    if constexpr (TRC) {                                                      \
+        const unsigned tn = (unsigned)__builtin_amdgcn_s_memrealtime();       \
+        acc += tn - tk;                                                       \
+        tk = tn;                                                              \
+    }
+    r2cw2_issue<P_TWS>(A, row, B, B - 8 * (j0 + o) - 8, a.tw, tid0); /* hi of the first tile */
 #pragma unroll 1
     for (unsigned jr = 0; jr < len; jr++) {
         unsigned tid = tid0;
@@ -559,24 +581,27 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
         const unsigned g = tid & 7, jt = tid >> 3;
         const unsigned j = j0 + (o + jr) % len;
         const unsigned qlo = 8 * j + 1;
-        r2cw2_issue(Bf, row, B, qlo, a.tw, tid); /* lo(j) loads while hi(j) is transformed */
+        r2cw2_issue<P_TWS>(Bf, row, B, qlo, a.tw, tid); /* lo(j) loads while hi(j) is transformed */
         double2 w2[7];
         /* ---- hi(j), in place in A */
         r2cw2_tw(A, w2, lds, ltw, tid);
         r2c_stages<SGN, false>(A.r, A.i, w2, lds, ltw, tid);
+        R2C_MARK(tr1)
         double him[8];
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) him[jj] = A.i[jj];
         /* ---- lo(j), in place in Bf */
         r2cw2_tw(Bf, w2, lds, ltw, tid);
+
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) ld[4096 + (jt + jj * TPG) * G + g] = A.r[jj]; /* hi real parts wait here */
         {   /* the next tile's hi loads while lo(j) is transformed; unconditional (the last tile
              * reloads itself) */
             const unsigned jn = jr + 1 < len ? j0 + (o + jr + 1) % len : j;
-            r2cw2_issue(A, row, B, B - 8 * jn - 8, a.tw, tid);
+            r2cw2_issue<P_TWS>(A, row, B, B - 8 * jn - 8, a.tw, tid);
         }
         r2c_stages<SGN, true>(Bf.r, Bf.i, w2, lds, ltw, tid);
+        R2C_MARK(tr2)
         __syncthreads();
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
@@ -589,8 +614,10 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
             const unsigned sl = (P - 1 - u) * G + (7 - g);
             const double2 zk = make_double2(Bf.r[jj], Bf.i[jj]), zh = make_double2(ld[4096 + sl], ld[sl]);
             double re, im, re2, im2;
-            r8::r2c_pair(zk, zh, w2t[k], re, im);
-            r8::r2c_pair(zh, zk, w2t[hk], re2, im2);
+            const double2 wk = P_TW2 ? w2t[tid0 & 63] : w2t[k];
+            const double2 whk = P_TW2 ? w2t[(tid0 & 63) + 64] : w2t[hk];
+            r8::r2c_pair(zk, zh, wk, re, im);
+            r8::r2c_pair(zh, zk, whk, re2, im2);
             X[N - k] = make_double2(re, -im);
             X[hk] = make_double2(re2, im2);
             const double2 va = grp_shift<-1>(make_double2(re, im)), vb = grp_shift<-1>(make_double2(re2, -im2));
@@ -610,6 +637,15 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
                 cry[512 + u] = vb;
             }
         }
+        R2C_MARK(tr3)
+    }
+#undef R2C_MARK
+    if (TRC && tid0 == 0) {
+        unsigned *d = a.dbg + blockIdx.x * 4;
+        d[0] = len;
+        d[1] = tr1;
+        d[2] = tr2;
+        d[3] = tr3;
     }
     /* the last chain's carry: bin 8*(j0+o), or 8*j1 without rotation (at the row's last tile,
      * column B/2, already written by the aligned streams) */
@@ -656,11 +692,51 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         const long long T = env("HSFFT_R2C_WT", 8) > 0 ? env("HSFFT_R2C_WT", 8) : 8, W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
-        void (*fw)(Args, unsigned, unsigned, unsigned) = sgn == 1 ? k_r2c_walk2<1> : k_r2c_walk2<-1>;
+        /* HSFFT_R2C_NT (measurement): bit 0 non-temporal data loads, bit 1 non-temporal stores */
+        typedef void (*wfn)(Args, unsigned, unsigned, unsigned);
+        const bool dbg = env("HSFFT_R2C_DEBUG", 0) != 0; /* the traced default variant */
+#ifdef HSFFT_DEV_PROBES
+        /* HSFFT_R2C_PROBE (timing only, results wrong): 1 no twiddle2 traffic, 2 no stage-2
+         * twiddle traffic, 3 neither */
+        static const wfn fws[2][8] = {
+            {k_r2c_walk2<1, 0>, k_r2c_walk2<1, 1>, k_r2c_walk2<1, 2>, k_r2c_walk2<1, 3>, k_r2c_walk2<1, 4>,
+             k_r2c_walk2<1, 5>, k_r2c_walk2<1, 6>, k_r2c_walk2<1, 7>},
+            {k_r2c_walk2<-1, 0>, k_r2c_walk2<-1, 1>, k_r2c_walk2<-1, 2>, k_r2c_walk2<-1, 3>, k_r2c_walk2<-1, 4>,
+             k_r2c_walk2<-1, 5>, k_r2c_walk2<-1, 6>, k_r2c_walk2<-1, 7>}};
+        wfn fw = fws[sgn == 1 ? 0 : 1][(dbg ? 1 : 0) | (env("HSFFT_R2C_PROBE", 0) & 3) << 1];
+#else
+        static const wfn fws[2][2] = {{k_r2c_walk2<1, 0>, k_r2c_walk2<1, 1>}, {k_r2c_walk2<-1, 0>, k_r2c_walk2<-1, 1>}};
+        wfn fw = fws[sgn == 1 ? 0 : 1][dbg ? 1 : 0];
+#endif
+        const int lds_bytes = R2CW2_LDS;
         a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
-        HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, R2CW2_LDS));
-        hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), R2CW2_LDS, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
+        static unsigned *s_dbg = nullptr;
+        static long long s_dbg_n = 0;
+        if (dbg) {
+            if (s_dbg_n < grid) {
+                if (s_dbg) HCHK(hipFree(s_dbg));
+                HCHK(hipMalloc((void **)&s_dbg, (size_t)grid * 4 * sizeof(unsigned)));
+                s_dbg_n = grid;
+            }
+            HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 4 * sizeof(unsigned), st));
+            a.dbg = s_dbg;
+        }
+        HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+        hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), lds_bytes, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());
+        if (dbg) { /* mean us per tile pair of the walking workgroups */
+            unsigned *hb = (unsigned *)malloc((size_t)grid * 4 * sizeof(unsigned));
+            if (!hb) return -1;
+            HCHK(hipMemcpyAsync(hb, s_dbg, (size_t)grid * 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+            HCHK(hipStreamSynchronize(st));
+            double t[4] = {0, 0, 0, 0};
+            for (long long w = 0; w < grid; w++)
+                for (int i = 0; i < 4; i++) t[i] += hb[w * 4 + i];
+            free(hb);
+            const double n = t[0] > 0 ? t[0] : 1;
+            fprintf(stderr, "r2c_walk2: tile pairs %.0f  us per tile pair: hi %.2f lo %.2f pairs+stores %.2f\n", t[0],
+                    t[1] / n / 100.0, t[2] / n / 100.0, t[3] / n / 100.0);
+        }
         return 0;
     }
     const long long grid = a.tiles * (long long)batch;

@@ -26,6 +26,7 @@ struct Args {
     int xcd_groups;   /* >0: remap block ids so that consecutive tiles share an XCD */
     int tile_major;   /* 1: block order tile-major (all rows of a tile adjacent) */
     long long batch;
+    unsigned *dbg;    /* optional per-workgroup phase trace (k_r2c_walk2, HSFFT_R2C_DEBUG) */
 };
 
 template <int N>

@@ -599,8 +599,7 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
     length and a short last walk; 4096: one walk per row (the carry reaches column B/2);
     walk0: the one-tile-per-workgroup k_r2c_fused; o1 / o2: segment-major block order, o2 with
     the walk start rotated per row (two carry chains per walk), o3 / o5 / o9 with 2 / 4 / 8
-    evenly spaced rotation classes.  Bit-exact vs the oracle, odd
-    batch, stale output buffer."""
+    evenly spaced rotation classes.  Bit-exact vs the oracle, odd batch, stale output buffer."""
     if wt == "walk0":
         monkeypatch.setenv("HSFFT_R2C_WALK", "0")
     else:
