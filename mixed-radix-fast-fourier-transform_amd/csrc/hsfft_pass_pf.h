@@ -20,6 +20,15 @@
 
 namespace pf {
 
+#ifdef HSFFT_DEV_PROBES
+/* development build only (results WRONG when changed): mask on the k_local of the global
+ * L = 512 twiddles of a 4096-point first pass (HSFFT_PFA_PROBE=1: 7, i.e. one 7-entry run) */
+__device__ unsigned pf_probe_twmask = 0xffffffffu;
+#define PF_TWMASK pf_probe_twmask
+#else
+#define PF_TWMASK 0xffffffffu
+#endif
+
 using r8::Args;
 using r8::Shape;
 
@@ -136,7 +145,7 @@ __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], dou
         stage<8, SGN>(xr, xi, w, false);
     }
     if constexpr (N8 >= 3) {
-        if constexpr (TWG) tw8<CONJ>(w, gtw, S::Lloc(3), jt & (S::Lloc(3) - 1));
+        if constexpr (TWG) tw8<CONJ>(w, gtw, S::Lloc(3), jt & (S::Lloc(3) - 1) & PF_TWMASK);
         r8::exchange<8, S::Lloc(2), 8, TPG, P, G, true>(xr, xi, lds, jt, g);
         if constexpr (!TWG) tw8_lds<CONJ>(w, ltw, S::Lloc(3), jt & (S::Lloc(3) - 1));
         stage<8, SGN>(xr, xi, w, false);
@@ -505,8 +514,10 @@ constexpr int R2CW2_LDS = (512 * 8 + 504 + 1024) * 16;
  * non-temporal data loads and / or output stores (c5 88.3 / 91.3 / 85.2 vs 95.1-96.2 on one
  * box); the lo tile's twiddle2 prefetched by LDS-DMA and the hi tile's into registers during
  * the lo stages (bit-exact, 228 VGPRs: 104.6-105.0 vs 105.3-105.7 -- the wait moves from the
- * pairs phase to the lo phase).  Probes: with no twiddle traffic at all c5 gains 2.5 %
- * (108.3 / 107.7 vs 105.7 / 105.3): the twiddle re-reads are not what bounds the walk. */
+ * pairs phase to the lo phase); one output stream (X[N-k]) parked in LDS and stored during the
+ * next tile's hi phase (bit-exact, 209 VGPRs, 152 KiB LDS: 103.0-103.2 vs 102.4-103.6 -- the
+ * pairs phase sheds 0.7 us, the hi phase gains 2.1).  Probes: with no twiddle traffic at all c5
+ * gains 2.5 % (108.3 / 107.7 vs 105.7 / 105.3): the twiddle re-reads are not what bounds the walk. */
 template <int SGN, int V = 0>
 __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsigned T, unsigned W)
 {
@@ -820,6 +831,12 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     size_t lds = 0;
     kfn fn = pick(p, l, &G, &TL, &threads, &lds);
     if (!fn) return 1;
+#ifdef HSFFT_DEV_PROBES
+    {
+        const unsigned m = env("HSFFT_PFA_PROBE", 0) ? 7u : 0xffffffffu;
+        HCHK(hipMemcpyToSymbol(HIP_SYMBOL(pf_probe_twmask), &m, sizeof m));
+    }
+#endif
     Args a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)l->in;
