@@ -1,0 +1,18 @@
+#!/bin/bash
+# round-3 GPU session X: r2c split walk with the hi tiles' points prefetched two tiles ahead by
+# LDS-DMA (HSFFT_R2C_PF2=1): parity, phase trace, three interleaved timing passes
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+one() { grep '^{' "$1" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$2', d['value'], d['ms_per_step'], r['frac'], d.get('stream_copy_gbs'), d.get('placement',{}).get('copy_gbs'))"; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "r2c_walk" > gpurun_out/pytest_r3x.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_r3x.log
+case $rc in 0) ;; *) exit $rc;; esac
+HSFFT_R2C_PF2=1 HSFFT_R2C_DEBUG=1 timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --steps 1 --warmup 0 > gpurun_out/x_c5_trace.log 2>&1 || exit $?
+grep 'r2c_walk2:' gpurun_out/x_c5_trace.log | tail -1
+for pass in 1 2 3; do
+  for pk in 0 1; do
+    HSFFT_R2C_PF2=$pk timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/x_c5_pf2${pk}_$pass.log 2>&1 || exit $?
+    one gpurun_out/x_c5_pf2${pk}_$pass.log "c5 pf2=$pk pass=$pass"
+  done
+done
+exit 0
