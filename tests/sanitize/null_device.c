@@ -17,11 +17,26 @@
 
 static __thread char err[256];
 static __thread int sidx;
-static volatile double sink;
+static __thread volatile double sink; /* per thread: launches on different null devices run concurrently */
 
-int hsd_device_count(void) { return 1; }
-int hsd_set_device(int dev) { return dev == 0 ? 0 : -1; }
-int hsd_get_device(void) { return 0; }
+/* HSFFT_NULL_NDEV (default 1) null devices, so that the multi-device paths
+ * (hsfft_exec_multi: one host thread per device, per-device state, locks and scratch) run
+ * under the sanitizers on a machine with no GPU; the current device is per thread and starts
+ * at 0, as in HIP */
+static __thread int cur_dev;
+int hsd_device_count(void)
+{
+    const char *e = getenv("HSFFT_NULL_NDEV");
+    const int n = e ? atoi(e) : 1;
+    return n < 1 ? 1 : n > 16 ? 16 : n;
+}
+int hsd_set_device(int dev)
+{
+    if (dev < 0 || dev >= hsd_device_count()) return -1;
+    cur_dev = dev;
+    return 0;
+}
+int hsd_get_device(void) { return cur_dev; }
 void *hsd_malloc(size_t bytes) { return malloc(bytes ? bytes : 16); }
 int hsd_free(void *p)
 {

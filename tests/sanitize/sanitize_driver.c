@@ -12,7 +12,10 @@
  *      hsfft_release_scratch -- the null device touches the first and last element of every
  *      row each launch would read or write;
  *   3. threads: 8 host threads creating / executing / freeing plans, sharing one plan, and
- *      cycling convolutions through more padded lengths than the plan cache holds.
+ *      cycling convolutions through more padded lengths than the plan cache holds;
+ *   4. devices: hsfft_exec_multi over the 4 null devices the test asks for (HSFFT_NULL_NDEV):
+ *      one host thread per device building its own device state, shards of uneven size, two
+ *      callers at once, then free_fft releasing the state of every device.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -122,6 +125,25 @@ static void run_conv(int n, int m)
 
 static fft_object g_shared;
 
+/* 4. two callers running hsfft_exec_multi on one shared plan at once */
+static fft_object g_multi;
+static void *multi_caller(void *arg)
+{
+    const int ndev = hsfft_device_count(), n = 12600, rows = 5 + (int)(long)arg;
+    const fft_data *ins[16];
+    fft_data *outs[16];
+    for (int g = 0; g < ndev; g++) {
+        ins[g] = cbuf((long long)n * rows);
+        outs[g] = cbuf((long long)n * rows);
+    }
+    for (int it = 0; it < 4; it++) CHECK(hsfft_exec_multi(g_multi, ins, outs, rows, ndev) == 0, "concurrent exec_multi");
+    for (int g = 0; g < ndev; g++) {
+        free((void *)ins[g]);
+        free(outs[g]);
+    }
+    return NULL;
+}
+
 static void *hammer(void *arg)
 {
     const int t = (int)(long)arg;
@@ -196,6 +218,38 @@ int main(void)
     free(x);
     free(y);
     CHECK(hsfft_release_scratch() == 0, "release_scratch");
+
+    /* 4. hsfft_exec_multi over every null device (rows split unevenly: 7 over 4 devices) */
+    {
+        const int ndev = hsfft_device_count();
+        CHECK(ndev == 4, "null devices: %d (the test sets HSFFT_NULL_NDEV=4)", ndev);
+        const int msz[] = {1024, 12600, 99991, 1 << 18};
+        for (unsigned i = 0; i < sizeof msz / sizeof msz[0]; i++) {
+            const int n = msz[i], rows = 7;
+            fft_object o = fft_init(n, i & 1 ? -1 : 1);
+            const fft_data *ins[16];
+            fft_data *outs[16];
+            for (int g = 0; g < ndev; g++) {
+                const int r = rows * (g + 1) / ndev - rows * g / ndev;
+                ins[g] = cbuf((size_t)n * (r > 0 ? r : 1));
+                outs[g] = cbuf((size_t)n * (r > 0 ? r : 1));
+            }
+            CHECK(hsfft_exec_multi(o, ins, outs, rows, ndev) == 0, "exec_multi %d: %s", n, hsfft_last_error());
+            CHECK(hsfft_exec_multi(o, ins, outs, 2, ndev) == 0, "exec_multi %d, 2 rows over %d devices", n, ndev);
+            CHECK(hsfft_exec_multi(o, ins, outs, rows, ndev + 1) < 0, "exec_multi %d: more devices than exist", n);
+            free_fft(o);
+            for (int g = 0; g < ndev; g++) {
+                free((void *)ins[g]);
+                free(outs[g]);
+            }
+        }
+        CHECK(hsfft_get_device() == 0, "exec_multi restores the caller's device");
+        g_multi = fft_init(12600, -1);
+        pthread_t mt[2];
+        for (long t = 0; t < 2; t++) pthread_create(&mt[t], NULL, multi_caller, (void *)t);
+        for (int t = 0; t < 2; t++) pthread_join(mt[t], NULL);
+        free_fft(g_multi);
+    }
 
     g_shared = fft_init(12600, 1);
     pthread_t th[8];
