@@ -959,6 +959,9 @@ static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
  * built.  Returns 1 when the call does not qualify (then the locked path runs). */
 static __thread void *t_pin[HS_MAX_DEV][2];
 static __thread size_t t_pin_sz[HS_MAX_DEV];
+/* this thread's completion word per device (page-locked) and its sequence */
+static __thread unsigned *t_flag[HS_MAX_DEV];
+static __thread unsigned t_seq;
 
 static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *oup)
 {
@@ -994,11 +997,21 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
             return 1;
         }
     }
+    if (!t_flag[d] && env_int("HSFFT_SMALL_FLAG", 1)) t_flag[d] = (unsigned *)hsd_host_alloc(64);
     memcpy(t_pin[d][0], inp, bytes);
     hsd_select_stream(3);
     int rc = run_chain(e, ds, t_pin[d][0], obj->N, t_pin[d][1], obj->N, 1, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL,
                        HS_STORE_PLAIN, NULL, e->M);
-    if (!rc) rc = hsd_stream_sync();
+    if (!rc) {
+        /* the stream's completion seen through a host word instead of the stream wait
+         * (HSFFT_SMALL_FLAG=0: the wait) */
+        if (t_flag[d]) {
+            if (++t_seq == 0) t_seq = 1;
+            rc = hsd_stream_signal_wait(t_flag[d], t_seq);
+        } else {
+            rc = hsd_stream_sync();
+        }
+    }
     hsd_select_stream(0);
     hs_entry_put(e);
     if (rc) fatal("fft_exec failed");

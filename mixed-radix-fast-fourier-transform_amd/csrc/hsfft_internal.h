@@ -81,6 +81,9 @@ int hsd_select_stream(int idx);   /* 0 library stream, 1 pipeline / H2D, 2 D2H, 
 int hsd_h2d_async(void *d, const void *h, size_t bytes);   /* on the selected stream */
 int hsd_d2h_async(void *h, const void *d, size_t bytes);
 int hsd_stream_sync(void);        /* the selected stream */
+/* completion of the selected stream's work through a page-locked word the host polls
+ * (flag from hsd_host_alloc, v a fresh value), stream wait as the fallback */
+int hsd_stream_signal_wait(unsigned *flag, unsigned v);
 int hsd_host_register(void *p, size_t bytes);
 int hsd_host_unregister(void *p);
 void *hsd_host_alloc(size_t bytes);  /* page-locked, device-accessible host memory */

@@ -5,6 +5,9 @@
 //      the flag (no stream wait)
 //   c) kernel copying 16 KB from one page-locked host buffer to another (the zero-copy
 //      pattern of the small fft_exec path) + hipStreamSynchronize
+//   d) the same copy kernel followed by hipStreamWriteValue32 of a sequence number into
+//      page-locked host memory; the host polls that word (no stream wait)
+//   e) the same copy with the flag stored by the kernel itself after a system-scope fence
 // Build: hipcc -O2 --offload-arch=gfx950 c1_latency.hip -o c1_latency (binary git-ignored)
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -36,6 +39,16 @@ __global__ void k_copy(const double2 *in, double2 *out, int n)
     for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = in[i];
 }
 
+__global__ void k_copy_flag(const double2 *in, double2 *out, int n, volatile unsigned *flag, unsigned v)
+{
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = in[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        *flag = v;
+    }
+}
+
 static double med(std::vector<double> v)
 {
     std::sort(v.begin(), v.end());
@@ -54,7 +67,10 @@ int main()
     CK(hipHostMalloc((void **)&hout, 16384, hipHostMallocDefault));
     for (int i = 0; i < 1024; i++) hin[i] = make_double2(i, -i);
     const int R = 2000;
-    std::vector<double> ta, tb, tc;
+    std::vector<double> ta, tb, tc, td, te;
+    unsigned *flag2;
+    CK(hipHostMalloc((void **)&flag2, 64, hipHostMallocCoherent));
+    *(volatile unsigned *)flag2 = 0;
     for (int r = 0; r < R + 100; r++) {
         auto t0 = clk::now();
         hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st);
@@ -74,7 +90,31 @@ int main()
         hipLaunchKernelGGL(k_copy, dim3(1), dim3(256), 0, st, (const double2 *)hin, hout, 1024);
         CK(hipStreamSynchronize(st));
         auto t4 = clk::now();
+        auto t5 = clk::now();
+        hipLaunchKernelGGL(k_copy, dim3(1), dim3(256), 0, st, (const double2 *)hin, hout, 1024);
+        CK(hipStreamWriteValue32(st, flag2, (uint32_t)(r + 1), 0));
+        spins = 0;
+        while (__atomic_load_n(flag2, __ATOMIC_ACQUIRE) != (unsigned)(r + 1))
+            if (++spins > 2000000000L) {
+                fprintf(stderr, "write-value flag never arrived\n");
+                return 1;
+            }
+        auto t6 = clk::now();
+        CK(hipStreamSynchronize(st));
+        auto t7 = clk::now();
+        hipLaunchKernelGGL(k_copy_flag, dim3(1), dim3(256), 0, st, (const double2 *)hin, hout, 1024,
+                           (volatile unsigned *)flag, (unsigned)(r + 1000001));
+        spins = 0;
+        while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != (unsigned)(r + 1000001))
+            if (++spins > 2000000000L) {
+                fprintf(stderr, "kernel flag never arrived\n");
+                return 1;
+            }
+        auto t8 = clk::now();
+        CK(hipStreamSynchronize(st));
         if (r >= 100) {
+            td.push_back(std::chrono::duration<double, std::micro>(t6 - t5).count());
+            te.push_back(std::chrono::duration<double, std::micro>(t8 - t7).count());
             ta.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
             tb.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
             tc.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
@@ -84,7 +124,8 @@ int main()
         fprintf(stderr, "copy check failed\n");
         return 1;
     }
-    printf("median us: empty+sync %.2f | empty+host-flag poll %.2f | 16KB pinned->pinned copy kernel+sync %.2f\n",
-           med(ta), med(tb), med(tc));
+    printf("median us: empty+sync %.2f | empty+host-flag poll %.2f | 16KB pinned->pinned copy kernel+sync %.2f | "
+           "copy+writeValue poll %.2f | copy with in-kernel flag poll %.2f\n",
+           med(ta), med(tb), med(tc), med(td), med(te));
     return 0;
 }
