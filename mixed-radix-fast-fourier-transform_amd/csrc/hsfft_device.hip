@@ -813,6 +813,20 @@ int hsd_stream_sync(void)
  * with hipStreamSynchronize (tools/experiments/c1_latency.hip).  Falls back to the stream wait
  * after ~2 s without the value (a faulted queue never writes it; the wait then reports the
  * error). */
+/* wait for a kernel of the selected stream to store v into the host word (hsd_launch.done),
+ * stream wait as the fallback after ~2 s (a faulted kernel never stores it) */
+int hsd_host_word_wait(unsigned *flag, unsigned v)
+{
+    const unsigned long long t0 = (unsigned long long)clock();
+    for (unsigned long n = 0;; n++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+        if ((n & 0xFFFF) == 0xFFFF && (unsigned long long)clock() - t0 > 2ull * CLOCKS_PER_SEC) break;
+    }
+    HCHK(hipStreamSynchronize(stream()));
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) return set_err(hipErrorUnknown, "kernel completion word");
+    return 0;
+}
+
 int hsd_stream_signal_wait(unsigned *flag, unsigned v)
 {
     HCHK(hipStreamWriteValue32(stream(), flag, v, 0));

@@ -612,12 +612,24 @@ fail:
 }
 
 /* ------------------------------------------------------------------ pass chains */
+/* this thread's completion word for its next launch (small host-buffer path): set by the
+ * caller, consumed by launch_pass; t_done_armed says whether the kernel took it */
+static __thread unsigned *t_done;
+static __thread unsigned t_done_val;
+static __thread int t_done_armed;
+
 static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long long idist, void *out,
                        long long odist, int batch, int sgn, int conj, int dir, int load_op, const void *laux,
                        int store_op, const void *saux, long long nsig)
 {
     hsd_launch l;
     memset(&l, 0, sizeof l);
+    if (t_done) {
+        l.done = t_done;
+        l.done_val = t_done_val;
+        l.armed = &t_done_armed;
+        t_done = NULL;
+    }
     l.in = in;
     l.out = out;
     l.idist = idist;
@@ -997,20 +1009,28 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
             return 1;
         }
     }
-    if (!t_flag[d] && env_int("HSFFT_SMALL_FLAG", 1)) t_flag[d] = (unsigned *)hsd_host_alloc(64);
+    const int fmode = env_int("HSFFT_SMALL_FLAG", 2);
+    if (!t_flag[d] && fmode) t_flag[d] = (unsigned *)hsd_host_alloc(64);
     memcpy(t_pin[d][0], inp, bytes);
     hsd_select_stream(3);
+    if (t_flag[d]) {
+        if (++t_seq == 0) t_seq = 1;
+        t_done_armed = 0;
+        if (fmode >= 2) { /* a one-workgroup kernel stores the word itself */
+            t_done = t_flag[d];
+            t_done_val = t_seq;
+        }
+    }
     int rc = run_chain(e, ds, t_pin[d][0], obj->N, t_pin[d][1], obj->N, 1, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL,
                        HS_STORE_PLAIN, NULL, e->M);
+    t_done = NULL;
     if (!rc) {
-        /* the stream's completion seen through a host word instead of the stream wait
-         * (HSFFT_SMALL_FLAG=0: the wait) */
-        if (t_flag[d]) {
-            if (++t_seq == 0) t_seq = 1;
-            rc = hsd_stream_signal_wait(t_flag[d], t_seq);
-        } else {
-            rc = hsd_stream_sync();
-        }
+        /* completion seen through a host word instead of the stream wait: stored by the
+         * kernel (HSFFT_SMALL_FLAG=2, one-workgroup launches), else by the command processor
+         * after the kernel (1); 0: the stream wait */
+        if (t_flag[d] && t_done_armed) rc = hsd_host_word_wait(t_flag[d], t_seq);
+        else if (t_flag[d]) rc = hsd_stream_signal_wait(t_flag[d], t_seq);
+        else rc = hsd_stream_sync();
     }
     hsd_select_stream(0);
     hs_entry_put(e);

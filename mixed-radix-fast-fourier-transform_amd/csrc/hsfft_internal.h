@@ -63,6 +63,12 @@ typedef struct {
     const void *load_aux, *store_aux;
     long long nsig;
     int nt_load, nt_store;          /* non-temporal input / output (register kernels) */
+    /* completion word (small host-buffer calls): a kernel that runs as ONE workgroup stores
+     * done_val into *done (page-locked host memory) after every wave published its output at
+     * system scope, and the device layer sets *armed; other launches ignore it */
+    unsigned *done;
+    unsigned done_val;
+    int *armed;
 } hsd_launch;
 
 /* device layer (hsfft_device.hip) */
@@ -84,6 +90,8 @@ int hsd_stream_sync(void);        /* the selected stream */
 /* completion of the selected stream's work through a page-locked word the host polls
  * (flag from hsd_host_alloc, v a fresh value), stream wait as the fallback */
 int hsd_stream_signal_wait(unsigned *flag, unsigned v);
+/* the same for a word a kernel stores itself (hsd_launch.done) */
+int hsd_host_word_wait(unsigned *flag, unsigned v);
 int hsd_host_register(void *p, size_t bytes);
 int hsd_host_unregister(void *p);
 void *hsd_host_alloc(size_t bytes);  /* page-locked, device-accessible host memory */

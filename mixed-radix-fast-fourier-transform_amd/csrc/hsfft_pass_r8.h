@@ -27,6 +27,8 @@ struct Args {
     int tile_major;   /* 1: block order tile-major (all rows of a tile adjacent) */
     long long batch;
     unsigned *dbg;    /* optional per-workgroup phase trace (k_r2c_walk2, HSFFT_R2C_DEBUG) */
+    unsigned *done;   /* k_pass launched as one workgroup: host completion word (hsd_launch) */
+    unsigned done_val;
 };
 
 template <int N>
@@ -388,16 +390,25 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (occ_hint<R0, N8, G, FIRS
 
     /* last stage: ml == 0, output u = kloc + jj*LL, written to [m][u][q] */
     constexpr int RL = S::R(S::NST - 1), LL = S::Lloc(S::NST - 1), NBL = 8 / RL;
-    if (!valid) return;
+    if (valid) {
 #pragma unroll
-    for (int c = 0; c < NBL; c++) {
-        const int kloc = c * TPG + jt;
+        for (int c = 0; c < NBL; c++) {
+            const int kloc = c * TPG + jt;
 #pragma unroll
-        for (int jj = 0; jj < RL; jj++) {
-            const long long n = (m * P + kloc + jj * LL) * a.B + q;
-            if constexpr (HOOK) store_hook(a, out, n, xr[c * RL + jj], xi[c * RL + jj]);
-            else out[n] = make_double2(xr[c * RL + jj], xi[c * RL + jj]);
+            for (int jj = 0; jj < RL; jj++) {
+                const long long n = (m * P + kloc + jj * LL) * a.B + q;
+                if constexpr (HOOK) store_hook(a, out, n, xr[c * RL + jj], xi[c * RL + jj]);
+                else out[n] = make_double2(xr[c * RL + jj], xi[c * RL + jj]);
+            }
         }
+    }
+    if (a.done) { /* the launch is this one workgroup (host-checked): tell the host it is done --
+                   * every thread publishes its own stores at system scope, then one lane stores
+                   * the word (a release store at system scope) */
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -795,6 +806,13 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     a.tiles = tm * tq;
     const long long grid = a.tiles * l->batch;
     const int threads = (p->P / 8) * p->G;
+    a.done = nullptr;
+    a.done_val = 0;
+    if (l->done && l->armed && grid == 1) { /* one workgroup: it can signal its own completion */
+        a.done = l->done;
+        a.done_val = l->done_val;
+        *l->armed = 1;
+    }
     const size_t lds = (size_t)p->P * p->G * (split ? sizeof(double) : sizeof(double2));
     if (grid <= 0 || grid > 0x7fffffffLL || threads > 1024 || lds > 160 * 1024) {
         snprintf(g_err, sizeof g_err, "r8: bad geometry grid=%lld threads=%d lds=%zu", grid, threads, lds);

@@ -73,6 +73,12 @@ int hsd_select_stream(int idx)
 int hsd_h2d_async(void *d, const void *h, size_t bytes) { return hsd_h2d(d, h, bytes); }
 int hsd_d2h_async(void *h, const void *d, size_t bytes) { return hsd_d2h(h, d, bytes); }
 int hsd_stream_sync(void) { return 0; }
+int hsd_host_word_wait(unsigned *flag, unsigned v)
+{
+    (void)flag;
+    (void)v;
+    return 0; /* never armed on the null device */
+}
 int hsd_stream_signal_wait(unsigned *flag, unsigned v)
 {
     __atomic_store_n(flag, v, __ATOMIC_RELEASE); /* the null device completes at once */

@@ -154,6 +154,27 @@ def test_c2c_exact_twiddle_mode_every_length_2_to_8192():
     assert not bad, bad[:20]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("flag", ["2", "1", "0"])
+def test_c2c_dropin_repeated_calls_completion_word(flag, monkeypatch):
+    """back-to-back drop-in fft_exec calls on host buffers whose input changes every call, each
+    output checked bit-exact: the host reads the page-locked output slot as soon as the
+    completion word arrives (HSFFT_SMALL_FLAG=2: stored by the one-workgroup kernel itself
+    after every thread's system-scope release; 1: written by the command processor after the
+    kernel; 0: the stream wait) -- a word that overtook the data would show the PREVIOUS
+    call's output here.  Lengths whose pass is one workgroup (1024, 4096, 512) and one that is
+    not (12600: command-processor word)."""
+    monkeypatch.setenv("HSFFT_SMALL_FLAG", flag)
+    for n, calls in ((1024, 400), (4096, 150), (512, 300), (12600, 60)):
+        p = hsfft.Plan(n, 1)
+        xs = [T.complex_input(n, T.seed_for(n) ^ (0x5151 + c)) for c in range(calls)]
+        ys = [p.exec(x) for x in xs]
+        p.close()
+        ref = T.oracle_c2c(np.stack(xs), 1)
+        bad = [c for c in range(calls) if not T.bits_equal(ys[c], ref[c])]
+        assert not bad, (n, bad[:10])
+
+
 @pytest.mark.parametrize("concurrent", ["1", "0"])
 def test_c2c_dropin_every_length_2_to_4096(concurrent, monkeypatch):
     """the drop-in fft_exec on host buffers (one-pass plans take the page-locked zero-copy
