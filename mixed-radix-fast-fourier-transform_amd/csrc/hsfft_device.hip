@@ -815,12 +815,19 @@ int hsd_stream_sync(void)
  * error). */
 /* wait for a kernel of the selected stream to store v into the host word (hsd_launch.done),
  * stream wait as the fallback after ~2 s (a faulted kernel never stores it) */
+static double wall_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 int hsd_host_word_wait(unsigned *flag, unsigned v)
 {
-    const unsigned long long t0 = (unsigned long long)clock();
+    const double t0 = wall_s();
     for (unsigned long n = 0;; n++) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
-        if ((n & 0xFFFF) == 0xFFFF && (unsigned long long)clock() - t0 > 2ull * CLOCKS_PER_SEC) break;
+        if ((n & 0xFFFF) == 0xFFFF && wall_s() - t0 > 2.0) break;
     }
     HCHK(hipStreamSynchronize(stream()));
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) return set_err(hipErrorUnknown, "kernel completion word");
@@ -830,10 +837,10 @@ int hsd_host_word_wait(unsigned *flag, unsigned v)
 int hsd_stream_signal_wait(unsigned *flag, unsigned v)
 {
     HCHK(hipStreamWriteValue32(stream(), flag, v, 0));
-    const unsigned long long t0 = (unsigned long long)clock();
+    const double t0 = wall_s();
     for (unsigned long n = 0;; n++) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
-        if ((n & 0xFFFF) == 0xFFFF && (unsigned long long)clock() - t0 > 2ull * CLOCKS_PER_SEC) break;
+        if ((n & 0xFFFF) == 0xFFFF && wall_s() - t0 > 2.0) break;
     }
     HCHK(hipStreamSynchronize(stream()));
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) return set_err(hipErrorUnknown, "stream completion word");
