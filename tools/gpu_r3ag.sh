@@ -1,0 +1,27 @@
+#!/bin/bash
+# round-3 GPU session AG (third session): full GPU suite at HEAD (+ the 1024-thread 64-B-segment
+# c5 pass A variant, HSFFT_PFG=2), the default bench line, then c5 with PFG 1 / 2 interleaved
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_r3ag.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_r3ag.log
+case $rc in 0) ;; *) exit $rc;; esac
+timeout -k 10 600 python bench.py > gpurun_out/bench_default_r3ag.log 2>&1 || exit $?
+grep '^{' gpurun_out/bench_default_r3ag.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); r=d['roofline']
+    print('value', d['value'], 'ms', d['ms_per_step'], 'frac', r['frac'], 'pass_ms', r.get('pass_ms'), 'cpu', d['cpu_baseline']['value'], 'copy', d.get('stream_copy_gbs'), 'place', d.get('placement'))
+    for k,v in d.get('other_configs',{}).items(): print(' ', k, v.get('value'), v.get('unit'), v.get('frac'), (v.get('cpu_baseline') or {}).get('value'), (v.get('placement') or {}).get('copy_gbs'))
+"
+for rep in 1 2; do
+  for g in 1 2; do
+    HSFFT_PFG=$g timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --no-other-configs > gpurun_out/c5_pfg${g}_$rep.log 2>&1 || exit $?
+    grep '^{' gpurun_out/c5_pfg${g}_$rep.log | python3 -c "
+import json,sys
+d=json.loads(sys.stdin.readline()); r=d['roofline']
+print('c5 PFG=$g rep $rep', d['value'], 'ms', d['ms_per_step'], 'pass_ms', r.get('pass_ms'), 'place', (d.get('placement') or {}).get('copy_gbs'))
+"
+  done
+done
+exit 0
