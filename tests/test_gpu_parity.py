@@ -580,6 +580,40 @@ def test_power_of_two_sweep_both_signs(k):
         assert T.bits_equal(gpu_c2c_batched(n, sgn, x), oracle_rows(x, sgn)), (n, sgn)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,sgn", [(1 << 24, 1), (1 << 25, -1), (1 << 26, 1), (3 ** 14, -1), (5 ** 9, 1), (7 ** 8, 1),
+                                   (2 ** 6 * 3 ** 3 * 5 ** 2 * 7 ** 2, -1), (1000003, 1), (4194301, -1)])
+def test_largest_sizes_bit_exact(n, sgn):
+    """the largest single transforms (one row each): powers of two to 2^26 (1 GiB rows, chains
+    of three and more passes), long single-radix chains (3^14, 5^9, 7^8: the reference's D2
+    table quirk makes 3^14 / 7^8 numerically wrong, and the GPU reproduces those bits), a
+    2M-point mixed size, and Bluestein at M = 2^21 (prime 1000003) and M = 2^23 (prime 4194301,
+    the largest below 2^22) -- bit-exact vs the oracle (highSpeedFFT.c:1920-1942, :1735-1907)."""
+    x = T.complex_input(n, 0x1A7 ^ n)
+    y = gpu_c2c_batched(n, sgn, x.reshape(1, n)).reshape(n)
+    ref = oracle_rows(x, sgn)
+    assert T.bits_equal(y, ref), (n, sgn, T.mismatches(y, ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,sgn", [(1 << 26, 1), (1 << 24, -1), (2 * 1000003, 1), (2 * 12600 * 81, -1)])
+def test_largest_real_sizes_bit_exact(n, sgn):
+    """r2c at the largest sizes (one row): 2^26 reals (inner 2^25 c2c), a Bluestein inner
+    transform (N/2 = 1000003, M = 2^21) and a mixed-radix inner size -- bit-exact vs the oracle
+    (real.c:78-136)."""
+    x = T.real_input(n, 0x2B7 ^ n).reshape(1, n)
+    rp = hsfft.RealPlan(n, sgn)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(n * 16)
+    hsfft.r2c_batched(rp, din, dout, 1)
+    y = dout.to_array(np.complex128).reshape(1, n)
+    ref = T.oracle_r2c(x, sgn)
+    assert T.bits_equal(y, ref), (n, sgn, T.mismatches(y, ref))
+    din.free()
+    dout.free()
+    rp.close()
+
+
 def test_two_pass_2pow21_batched():
     """2^21 = [8,8,8,8] (4096-point first pass) + [8,8,8]: bit-exact vs the oracle."""
     n = 1 << 21
