@@ -33,11 +33,14 @@ int find_optimal_fft_length(int min_length, const char *conv_type, int length1, 
 }
 
 /* Plan cache: entries are reference counted -- a slot in use by any thread is never
- * evicted; when every slot is busy the call builds a private pair and frees it afterwards. */
+ * evicted; when every slot is busy the call builds a private pair and frees it afterwards.
+ * A slot being built carries its P and mode with `building` set: a concurrent request for the
+ * same length waits for that build instead of evicting another slot for a duplicate pair. */
 #define HS_CONV_CACHE 8
 static pthread_mutex_t g_clock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_cbuilt = PTHREAD_COND_INITIALIZER;
 static struct {
-    int P, mode, refs;
+    int P, mode, refs, building;
     unsigned long long used; /* LRU stamp */
     fft_real_object f, i;
 } g_cache[HS_CONV_CACHE];
@@ -53,28 +56,41 @@ static conv_pair conv_plans(int P)
     const int mode = hsfft_get_twiddle_mode();
     conv_pair cp = {NULL, NULL, -1};
     pthread_mutex_lock(&g_clock);
-    int victim = -1;
-    for (int k = 0; k < HS_CONV_CACHE; k++) {
-        if (g_cache[k].f && g_cache[k].P == P && g_cache[k].mode == mode) {
-            g_cache[k].refs++;
-            g_cache[k].used = ++g_cache_clock;
-            cp.f = g_cache[k].f;
-            cp.i = g_cache[k].i;
-            cp.slot = k;
-            pthread_mutex_unlock(&g_clock);
-            return cp;
+    for (;;) {
+        int victim = -1, pending = 0;
+        for (int k = 0; k < HS_CONV_CACHE; k++) {
+            const int same = g_cache[k].P == P && g_cache[k].mode == mode;
+            if (same && g_cache[k].building) {
+                pending = 1;
+                break;
+            }
+            if (same && g_cache[k].f) {
+                g_cache[k].refs++;
+                g_cache[k].used = ++g_cache_clock;
+                cp.f = g_cache[k].f;
+                cp.i = g_cache[k].i;
+                cp.slot = k;
+                pthread_mutex_unlock(&g_clock);
+                return cp;
+            }
+            if (g_cache[k].refs == 0 && !g_cache[k].building &&
+                (victim < 0 || !g_cache[k].f || (g_cache[victim].f && g_cache[k].used < g_cache[victim].used)))
+                victim = k;
         }
-        if (g_cache[k].refs == 0 && (victim < 0 || !g_cache[k].f || (g_cache[victim].f && g_cache[k].used < g_cache[victim].used)))
-            victim = k;
-    }
-    if (victim >= 0) { /* reserve the least recently used idle slot; build and free outside
-                        * the lock (plans of other lengths / devices are not held up) */
+        if (pending) { /* another thread is building this length: wait, then look again */
+            pthread_cond_wait(&g_cbuilt, &g_clock);
+            continue;
+        }
+        if (victim < 0) break;
+        /* reserve the least recently used idle slot; build and free outside the lock (plans
+         * of other lengths / devices are not held up) */
         fft_real_object of = g_cache[victim].f, oi = g_cache[victim].i;
         g_cache[victim].P = P;
         g_cache[victim].mode = mode;
         g_cache[victim].refs = 1;
+        g_cache[victim].building = 1;
         g_cache[victim].used = ++g_cache_clock;
-        g_cache[victim].f = g_cache[victim].i = NULL; /* building: no other thread matches it */
+        g_cache[victim].f = g_cache[victim].i = NULL;
         pthread_mutex_unlock(&g_clock);
         if (of) {
             free_real_fft(of);
@@ -84,8 +100,16 @@ static conv_pair conv_plans(int P)
         cp.i = fft_real_init(P, -1);
         cp.slot = victim;
         pthread_mutex_lock(&g_clock);
-        g_cache[victim].f = cp.f;
-        g_cache[victim].i = cp.i;
+        g_cache[victim].building = 0;
+        if (cp.f && cp.i) {
+            g_cache[victim].f = cp.f;
+            g_cache[victim].i = cp.i;
+        } else { /* failed build: the slot goes back empty, the caller keeps what it got */
+            g_cache[victim].P = 0;
+            g_cache[victim].refs = 0;
+            cp.slot = -1;
+        }
+        pthread_cond_broadcast(&g_cbuilt);
         pthread_mutex_unlock(&g_clock);
         return cp;
     }

@@ -648,10 +648,13 @@ int hsd_sync(void)
 
 /* wait for the library stream by polling an event (no blocking wait / wake-up): for short
  * synchronous calls (the small host-buffer fft_exec) */
+static thread_local hipEvent_t t_spin_ev[HS_MAX_DEV];
+static thread_local bool t_spin_have[HS_MAX_DEV];
+
 int hsd_sync_spin(void)
 {
-    static thread_local hipEvent_t ev[HS_MAX_DEV];
-    static thread_local bool have[HS_MAX_DEV];
+    hipEvent_t *ev = t_spin_ev;
+    bool *have = t_spin_have;
     const int dev = cur_dev();
     if (!have[dev]) {
         HCHK(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
@@ -780,6 +783,22 @@ int hsd_cu_count(void)
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
     return n;
+}
+
+void hsd_thread_release(void)
+{
+    for (int d = 0; d < HS_MAX_DEV; d++) {
+        if (t_own[d]) {
+            (void)hipStreamSynchronize(t_own[d]);
+            (void)hipStreamDestroy(t_own[d]);
+            t_own[d] = 0;
+        }
+        if (t_spin_have[d]) {
+            (void)hipEventDestroy(t_spin_ev[d]);
+            t_spin_have[d] = false;
+        }
+    }
+    (void)hipGetLastError();
 }
 
 int hsd_select_stream(int idx)

@@ -332,13 +332,27 @@ static void free_devstate(hs_devstate *d)
     free(d);
 }
 
+/* drop a device state that is being replaced: freed now, or by its last pinned user */
+static void retire_devstate(hs_devstate *d)
+{
+    if (!d) return;
+    if (d->refs > 0) d->retired = 1;
+    else free_devstate(d);
+}
+
+/* (device lock held) release a pin taken by the concurrent small path */
+static void devstate_put(hs_devstate *d)
+{
+    if (d && --d->refs == 0 && d->retired) free_devstate(d);
+}
+
 static void entry_free(hs_entry *e)
 {
     int cur = hsd_get_device();
     for (int d = 0; d < HS_MAX_DEV; d++)
         if (e->ds[d]) {
             hsd_set_device(d);
-            free_devstate(e->ds[d]);
+            retire_devstate(e->ds[d]);
         }
     if (cur >= 0) hsd_set_device(cur);
     free(e->tw_private);
@@ -563,8 +577,10 @@ static hs_devstate *devstate(hs_entry *e)
         hs_seterr("invalid current device %d", d);
         return NULL;
     }
-    if (e->ds[d] && e->ds_version[d] == e->version) return e->ds[d];
-    free_devstate(e->ds[d]);
+    /* bumped by hsfft_plan_refresh from any thread, read here under the device lock: atomic */
+    const int ver = __atomic_load_n(&e->version, __ATOMIC_ACQUIRE);
+    if (e->ds[d] && e->ds_version[d] == ver) return e->ds[d];
+    retire_devstate(e->ds[d]); /* a concurrent small call may still hold it */
     e->ds[d] = NULL;
     hs_devstate *s = calloc(1, sizeof *s);
     const size_t twb = sizeof(fft_data) * (size_t)(e->M > 1 ? e->M : 1);
@@ -603,7 +619,7 @@ static hs_devstate *devstate(hs_entry *e)
         if (rc) goto fail;
     }
     e->ds[d] = s;
-    e->ds_version[d] = e->version;
+    e->ds_version[d] = ver;
     return s;
 fail:
     if (!g_errbuf[0]) hs_seterr("device state: %s", hsd_errstr());
@@ -975,6 +991,34 @@ static __thread size_t t_pin_sz[HS_MAX_DEV];
 static __thread unsigned *t_flag[HS_MAX_DEV];
 static __thread unsigned t_seq;
 
+/* Per-thread resources (page-locked slots, completion words, the thread's own streams) are
+ * released when the thread exits: a pthread key whose destructor runs in the exiting thread,
+ * so callers that recycle or spawn threads do not leak pinned memory or streams. */
+static pthread_key_t g_tkey;
+static pthread_once_t g_tkey_once = PTHREAD_ONCE_INIT;
+
+static void thread_resources_free(void *unused)
+{
+    (void)unused;
+    for (int d = 0; d < HS_MAX_DEV; d++) {
+        hsd_host_free(t_pin[d][0]);
+        hsd_host_free(t_pin[d][1]);
+        hsd_host_free(t_flag[d]);
+        t_pin[d][0] = t_pin[d][1] = NULL;
+        t_pin_sz[d] = 0;
+        t_flag[d] = NULL;
+    }
+    hsd_thread_release();
+}
+
+static void tkey_init(void) { pthread_key_create(&g_tkey, thread_resources_free); }
+
+static void thread_resources_used(void)
+{
+    pthread_once(&g_tkey_once, tkey_init);
+    if (!pthread_getspecific(g_tkey)) pthread_setspecific(g_tkey, (void *)1);
+}
+
 static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *oup)
 {
     if (obj == NULL || inp == NULL || oup == NULL || (obj->lt != 0 && obj->lt != 1)) return 1; /* locked path reports */
@@ -993,11 +1037,13 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
     }
     hs_lock_device(); /* the plan's device state is built once, under the lock */
     hs_devstate *ds = devstate(e);
+    if (ds) ds->refs++; /* pinned until this call has completed (a refresh retires, never frees it) */
     hs_unlock_device(d);
     if (!ds) {
         hs_entry_put(e);
         return 1;
     }
+    thread_resources_used();
     if (t_pin_sz[d] < bytes) {
         hsd_host_free(t_pin[d][0]);
         hsd_host_free(t_pin[d][1]);
@@ -1005,17 +1051,21 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
         t_pin[d][1] = hsd_host_alloc(bytes);
         t_pin_sz[d] = t_pin[d][0] && t_pin[d][1] ? bytes : 0;
         if (!t_pin_sz[d]) {
+            hs_lock_device();
+            devstate_put(ds);
+            hs_unlock_device(d);
             hs_entry_put(e);
             return 1;
         }
     }
     const int fmode = env_int("HSFFT_SMALL_FLAG", 2);
     if (!t_flag[d] && fmode) t_flag[d] = (unsigned *)hsd_host_alloc(64);
+    const int use_flag = fmode >= 1 && t_flag[d] != NULL; /* the mode of THIS call, not of the first */
     memcpy(t_pin[d][0], inp, bytes);
     hsd_select_stream(3);
-    if (t_flag[d]) {
+    t_done_armed = 0;
+    if (use_flag) {
         if (++t_seq == 0) t_seq = 1;
-        t_done_armed = 0;
         if (fmode >= 2) { /* a one-workgroup kernel stores the word itself */
             t_done = t_flag[d];
             t_done_val = t_seq;
@@ -1028,11 +1078,15 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
         /* completion seen through a host word instead of the stream wait: stored by the
          * kernel (HSFFT_SMALL_FLAG=2, one-workgroup launches), else by the command processor
          * after the kernel (1); 0: the stream wait */
-        if (t_flag[d] && t_done_armed) rc = hsd_host_word_wait(t_flag[d], t_seq);
-        else if (t_flag[d]) rc = hsd_stream_signal_wait(t_flag[d], t_seq);
+        if (use_flag && t_done_armed) rc = hsd_host_word_wait(t_flag[d], t_seq);
+        else if (use_flag) rc = hsd_stream_signal_wait(t_flag[d], t_seq);
         else rc = hsd_stream_sync();
     }
+    if (rc) hsd_stream_sync(); /* nothing of this call may still run when the pin is dropped */
     hsd_select_stream(0);
+    hs_lock_device();
+    devstate_put(ds);
+    hs_unlock_device(d);
     hs_entry_put(e);
     if (rc) fatal("fft_exec failed");
     memcpy(oup, t_pin[d][1], bytes);
@@ -1064,9 +1118,7 @@ int hsfft_plan_refresh(fft_object obj)
     if (!obj) return HSFFT_ERR_ARG;
     hs_entry *e = hs_entry_get(obj);
     if (!e) return HSFFT_ERR_ARG;
-    pthread_mutex_lock(&g_lock);
-    e->version++;
-    pthread_mutex_unlock(&g_lock);
+    __atomic_fetch_add(&e->version, 1, __ATOMIC_ACQ_REL);
     hs_entry_put(e);
     return 0;
 }

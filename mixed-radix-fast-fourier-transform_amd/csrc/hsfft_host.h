@@ -18,6 +18,11 @@ typedef struct hs_devstate {
     void *d_gcs;  /* odd-radix cos/sin constants */
     void *d_chirp;/* Bluestein chirp h(n), N complex */
     void *d_hk;   /* Bluestein spectrum of the scaled, mirrored chirp, M complex */
+    /* users outside the device lock (the concurrent small fft_exec path) pin the state for
+     * their whole call: a rebuild (hsfft_plan_refresh) then retires it instead of freeing it,
+     * and the last hs_devstate_put frees it.  Both fields change under the device lock. */
+    int refs;
+    int retired;
 } hs_devstate;
 
 /* schedule derived from the public plan fields (snapshot) */

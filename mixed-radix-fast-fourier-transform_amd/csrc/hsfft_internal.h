@@ -96,6 +96,9 @@ int hsd_host_register(void *p, size_t bytes);
 int hsd_host_unregister(void *p);
 void *hsd_host_alloc(size_t bytes);  /* page-locked, device-accessible host memory */
 int hsd_host_free(void *p);
+/* release the calling thread's own device objects (its per-device streams, polling events);
+ * called from the thread-exit destructor of the host side */
+void hsd_thread_release(void);
 int hsd_event_record(int i);      /* event ring (64 slots) on the selected stream */
 int hsd_event_wait(int i);
 void *hsd_stream(void);

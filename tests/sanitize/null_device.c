@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "hsfft_internal.h"
 
@@ -95,9 +96,34 @@ int hsd_host_free(void *p)
 int hsd_event_record(int i) { return i < 0 ? -1 : 0; }
 int hsd_event_wait(int i) { return i < 0 ? -1 : 0; }
 void *hsd_stream(void) { return NULL; }
+/* per-thread objects released at thread exit: counted, so the driver can check the
+ * destructor ran once per thread that used the concurrent small path */
+int null_thread_releases;
+void hsd_thread_release(void) { __atomic_fetch_add(&null_thread_releases, 1, __ATOMIC_RELAXED); }
 /* "device" memory is host memory here: pointers the tests pass as device buffers are
- * malloc'd, so every pointer counts as a device pointer */
-int hsd_is_device_ptr(const void *p) { return p != NULL; }
+ * malloc'd, so every pointer counts as a device pointer -- except the buffers a test marks
+ * as host buffers (null_mark_host), which take the host-pointer paths of fft_exec (the
+ * concurrent small path among them) */
+#define NULL_NHOST 64
+static const void *null_host[NULL_NHOST];
+void null_mark_host(const void *p, int on)
+{
+    for (int i = 0; i < NULL_NHOST; i++) {
+        const void *want = on ? NULL : p;
+        if (__atomic_load_n(&null_host[i], __ATOMIC_ACQUIRE) == want) {
+            const void *exp = want;
+            if (__atomic_compare_exchange_n(&null_host[i], &exp, on ? p : NULL, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+                return;
+        }
+    }
+}
+int hsd_is_device_ptr(const void *p)
+{
+    if (p == NULL) return 0;
+    for (int i = 0; i < NULL_NHOST; i++)
+        if (__atomic_load_n(&null_host[i], __ATOMIC_ACQUIRE) == p) return 0;
+    return 1;
+}
 const char *hsd_errstr(void) { return err; }
 int hsd_cu_count(void) { return 256; }
 
@@ -128,6 +154,10 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
         snprintf(err, sizeof err, "null device: bad pass geometry");
         return -1;
     }
+    /* a launch on a thread's own stream (the concurrent small fft_exec path) "runs" a little
+     * later, as a queued kernel would: the window in which another thread could free what it
+     * reads (tests the device-state pinning) */
+    if (sidx == 3) usleep(20);
     const long long M = (long long)p->P * p->A * p->B;
     const long long in_len = l->load_op == HS_LOAD_CHIRP ? l->nsig : M;
     const long long out_len = l->store_op == HS_STORE_CHIRP ? l->nsig : M;

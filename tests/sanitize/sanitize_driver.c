@@ -144,6 +144,31 @@ static void *multi_caller(void *arg)
     return NULL;
 }
 
+/* 5. the concurrent small fft_exec path (host buffers, outside the device lock) on a plan
+ * that another thread refreshes: the refresh rebuilds the device state while a small call may
+ * still be using the old one (it must be retired, not freed, until that call is
+ * done); both threads' per-thread slots and streams are released when they exit */
+extern void null_mark_host(const void *p, int on);
+extern int null_thread_releases;
+static fft_object g_small;
+
+static void *small_caller(void *arg)
+{
+    const int refresher = (int)(long)arg;
+    fft_data *x = cbuf(1024), *y = cbuf(1024);
+    null_mark_host(x, 1);
+    null_mark_host(y, 1);
+    for (int it = 0; it < 300; it++) {
+        if (refresher) CHECK(hsfft_plan_refresh(g_small) == 0, "refresh while small calls run");
+        fft_exec(g_small, x, y);
+    }
+    null_mark_host(x, 0);
+    null_mark_host(y, 0);
+    free(x);
+    free(y);
+    return NULL;
+}
+
 static void *hammer(void *arg)
 {
     const int t = (int)(long)arg;
@@ -249,6 +274,17 @@ int main(void)
         for (long t = 0; t < 2; t++) pthread_create(&mt[t], NULL, multi_caller, (void *)t);
         for (int t = 0; t < 2; t++) pthread_join(mt[t], NULL);
         free_fft(g_multi);
+    }
+
+    {
+        g_small = fft_init(1024, 1);
+        const int rel0 = __atomic_load_n(&null_thread_releases, __ATOMIC_RELAXED);
+        pthread_t st[4];
+        for (long t = 0; t < 4; t++) pthread_create(&st[t], NULL, small_caller, (void *)(t == 0 ? 1L : 0L));
+        for (int t = 0; t < 4; t++) pthread_join(st[t], NULL);
+        free_fft(g_small);
+        const int rel = __atomic_load_n(&null_thread_releases, __ATOMIC_RELAXED) - rel0;
+        CHECK(rel == 4, "per-thread resources released at thread exit: %d of 4 threads", rel);
     }
 
     g_shared = fft_init(12600, 1);
