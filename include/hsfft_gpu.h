@@ -94,6 +94,10 @@ int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
 int hsfft_time_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out,
                            int batch, int iters, float *ms);
 
+/* Number of 8-byte words that differ between two device buffers of `bytes` bytes (a multiple
+ * of 8) into *count; synchronous.  For whole-output comparisons between schedules (tests). */
+int hsfft_count_diff_words(const void *d_a, const void *d_b, size_t bytes, uint64_t *count);
+
 /* Stream-copy reference: `iters` device copies of `bytes` (multiple of 16) from d_src to
  * d_dst, event-timed; the practical HBM ceiling reported next to the FFT numbers. */
 int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms);

@@ -524,6 +524,25 @@ __global__ __launch_bounds__(256) void k_copyU(const v2d *__restrict__ a, v2d *_
     }
 }
 
+/* differing 8-byte words (whole-buffer comparisons between schedules): one 64-bit
+ * agent-scope atomic add per workgroup after a wave / workgroup reduction */
+__global__ __launch_bounds__(256) void k_count_diff(const unsigned long long *__restrict__ a,
+                                                    const unsigned long long *__restrict__ b, long long n,
+                                                    unsigned long long *cnt)
+{
+    __shared__ unsigned long long part[4];
+    unsigned long long c = 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        c += a[i] != b[i];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = part[0] + part[1] + part[2] + part[3];
+        if (t) atomicAdd(cnt, t);
+    }
+}
+
 hipEvent_t g_t0[HS_MAX_DEV], g_t1[HS_MAX_DEV];
 hipEvent_t g_pev[HS_MAX_DEV][2 * HS_MAX_PASSES];
 std::atomic<bool> g_timer_init[HS_MAX_DEV];
@@ -774,6 +793,21 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         snprintf(g_err, sizeof g_err, "hsd_blue_xcd: an in-launch wait timed out (error word %u)", err);
         return 2;
     }
+    return 0;
+}
+
+int hsd_count_diff(const void *a, const void *b, long long nwords, unsigned long long *count)
+{
+    unsigned long long *d = nullptr;
+    HCHK(hipMalloc((void **)&d, sizeof *d));
+    HCHK(hipMemsetAsync(d, 0, sizeof *d, stream()));
+    if (nwords > 0)
+        hipLaunchKernelGGL(k_count_diff, dim3(8192), dim3(256), 0, stream(), (const unsigned long long *)a,
+                           (const unsigned long long *)b, nwords, d);
+    HCHK(hipGetLastError());
+    HCHK(hipMemcpyAsync(count, d, sizeof *d, hipMemcpyDeviceToHost, stream()));
+    HCHK(hipStreamSynchronize(stream()));
+    HCHK(hipFree(d));
     return 0;
 }
 

@@ -1322,6 +1322,19 @@ int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, fl
     return rc;
 }
 
+int hsfft_count_diff_words(const void *d_a, const void *d_b, size_t bytes, uint64_t *count)
+{
+    if (!d_a || !d_b || !count || bytes % 8) return HSFFT_ERR_ARG;
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    const int d = hs_lock_device();
+    unsigned long long c = 0;
+    rc = hsd_count_diff(d_a, d_b, (long long)(bytes / 8), &c) ? HSFFT_ERR_DEVICE : 0;
+    hs_unlock_device(d);
+    *count = c;
+    return rc;
+}
+
 /* one host thread per device: each selects its device, enqueues its contiguous shard and
  * waits for it; no data crosses devices.  Per-device state (twiddles, Bluestein hk) is built
  * by that device's thread, so first use builds all devices' state concurrently. */

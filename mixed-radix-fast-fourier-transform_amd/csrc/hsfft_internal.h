@@ -147,6 +147,8 @@ int hsd_copy_rows(const void *src, long long sdist, long long soff, long long nc
                   long long dlen, int batch);
 
 int hsd_cu_count(void);
+/* differing 8-byte words of two device buffers (synchronous) */
+int hsd_count_diff(const void *a, const void *b, long long nwords, unsigned long long *count);
 
 /* timing on the library stream */
 int hsd_timer_start(void);

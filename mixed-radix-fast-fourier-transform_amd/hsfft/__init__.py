@@ -67,6 +67,7 @@ SIGNATURES = {
     "hsfft_exec_multi": (CI, [VP, VP, VP, CI, CI]),
     "hsfft_bench_copy": (CI, [VP, VP, ctypes.c_size_t, CI, ctypes.POINTER(ctypes.c_float)]),
     "hsfft_bluestein_fallbacks": (ctypes.c_longlong, []),
+    "hsfft_count_diff_words": (CI, [VP, VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 STRUCT_TWIDDLE_OFFSET = 272  # offsetof(struct fft_set, twiddle), include/highspeedFFT.h
@@ -281,6 +282,13 @@ def bench_copy(d_src, d_dst, nbytes, iters):
     ms = ctypes.c_float(0.0)
     check(lib().hsfft_bench_copy(VP(d_src.ptr), VP(d_dst.ptr), nbytes, iters, ctypes.byref(ms)), "bench_copy")
     return ms.value
+
+
+def count_diff_words(d_a, d_b, nbytes):
+    """8-byte words that differ between two device buffers (on the GPU)"""
+    c = ctypes.c_uint64(0)
+    check(lib().hsfft_count_diff_words(VP(d_a.ptr), VP(d_b.ptr), nbytes, ctypes.byref(c)), "count_diff_words")
+    return c.value
 
 
 def time_r2c_batched(rplan, d_in, d_out, batch, iters):

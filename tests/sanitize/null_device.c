@@ -126,6 +126,13 @@ int hsd_is_device_ptr(const void *p)
 }
 const char *hsd_errstr(void) { return err; }
 int hsd_cu_count(void) { return 256; }
+int hsd_count_diff(const void *a, const void *b, long long nwords, unsigned long long *count)
+{
+    unsigned long long c = 0;
+    for (long long i = 0; i < nwords; i++) c += ((const uint64_t *)a)[i] != ((const uint64_t *)b)[i];
+    *count = c;
+    return 0;
+}
 
 /* read the first and last element of `rows` rows of `len` complex, `dist` apart */
 static void touch_rows_r(const void *base, long long dist, long long len, long long rows, size_t esz)
