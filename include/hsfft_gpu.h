@@ -103,9 +103,13 @@ int hsfft_count_diff_words(const void *d_a, const void *d_b, size_t bytes, uint6
 int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms);
 
 /* Bluestein M = 2^18 (e.g. N = 99991) runs as one persistent launch whose workgroups must all
- * be resident; when something else holds CUs its in-launch waits time out and the rows are
- * re-run on the three-launch path (same results, more time).  Count of such re-runs in this
- * process. */
+ * be resident at once; it is launched cooperatively, so the runtime refuses a grid that cannot
+ * be co-resident and the rows run on the three-launch path at once (same results, more time).
+ * Count of such calls in this process.  The launch is asynchronous like every batched call;
+ * its in-launch waits keep a last-resort bound (~1.3 s without progress), and a wait that
+ * still times out makes the next hsfft_synchronize() return HSFFT_ERR_DEVICE (the Bluestein
+ * outputs since the previous synchronisation are invalid).  HSFFT_BX_SYNC=1: each Bluestein
+ * call is synchronous and re-runs the rows of a timed-out launch itself. */
 long long hsfft_bluestein_fallbacks(void);
 
 /* --- threading -------------------------------------------------------------------------

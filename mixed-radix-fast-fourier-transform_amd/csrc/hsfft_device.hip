@@ -648,14 +648,23 @@ static unsigned *g_pl_ctr[HS_MAX_DEV];
 static size_t g_pl_bytes[HS_MAX_DEV];
 static unsigned *g_pl_err_host[HS_MAX_DEV];
 
-/* the sticky error word of the last persistent launch (set when a wait timed out) */
+/* The sticky error word of the persistent launches since the last check (set on the device
+ * when an in-launch wait timed out; copied to the pinned host word behind every launch, on the
+ * launch's stream).  Called after a synchronisation of that stream: reports the error once and
+ * clears both copies. */
 static int pl_check(void)
 {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV || !g_pl_err_host[dev]) return 0;
     if (*(volatile unsigned *)g_pl_err_host[dev] == 0) return 0;
     *g_pl_err_host[dev] = 0;
-    snprintf(g_err, sizeof g_err, "persistent launch: an in-launch dependency wait timed out (results invalid)");
+    if (g_pl_ctr[dev]) {
+        (void)hipMemsetAsync(g_pl_ctr[dev] + 8, 0, sizeof(unsigned), primary());
+        (void)hipStreamSynchronize(primary());
+    }
+    snprintf(g_err, sizeof g_err,
+             "persistent Bluestein launch: an in-launch dependency wait timed out; the outputs of the Bluestein "
+             "calls since the last synchronisation are invalid (HSFFT_BX_SYNC=1 re-runs such rows automatically)");
     return -2;
 }
 
@@ -689,11 +698,15 @@ int hsd_sync_spin(void)
 }
 
 /* Bluestein M = 2^18 as one persistent launch (hsfft_blue_xcd.h).  img: ng x 4 x M points of
- * scratch.  Synchronous: the launch is followed by a stream synchronisation and a check of its
- * error word.  Returns 0 on success, 1 if not applicable (geometry, or the grid would not be
- * co-resident), 2 if an in-launch wait timed out (the workgroups were not all resident, e.g.
- * another kernel held CUs: the caller re-runs the rows on the three-launch path), < 0 on a
- * HIP error. */
+ * scratch.  The grid is launched COOPERATIVELY (hipLaunchCooperativeKernel): the runtime
+ * checks at launch that every workgroup can be resident at once and refuses the launch
+ * otherwise (returned as 1: the caller runs the three-launch path at once).
+ * Asynchronous by default: the launch is queued on the library stream with a copy of its sticky
+ * error word behind it; a wait that still timed out (the last-resort bound, ~1.3 s without
+ * progress) is reported by the next hsfft_synchronize().  HSFFT_BX_SYNC=1: synchronous, and a
+ * timed-out launch returns 2 so the caller re-runs its rows on the three-launch path.
+ * Returns 0 on success (queued), 1 if not applicable, 2 (sync mode) if an in-launch wait timed
+ * out, 3 if the cooperative launch was refused, < 0 on a HIP error. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
                  const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng)
 {
@@ -706,27 +719,23 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     void (*fn)(bxc::XArgs) = sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>;
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bxc::LDS_BYTES));
     const int grid = ng * (int)bxc::NTILE;
-    {
-        /* every workgroup of a group must be resident at once (they wait on each other) */
-        int per_cu = 0, cus = 0;
-        HCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, 512, bxc::LDS_BYTES));
-        HCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        if ((long long)per_cu * cus < grid) return 1;
-    }
     /* counter block: [0, 32) the sticky error word (word 8) on its own line, then 2 counters
-     * per group, each on a 128-B line; zeroed as a whole (from the allocation's start, a
-     * multiple of 16 B: Guideline 16, re-initialise every call) before every launch */
+     * per group, each on a 128-B line; the counters are zeroed before every launch (Guideline
+     * 16, re-initialise every call), the error word only when it is reported (pl_check) */
     const size_t CS = bxc::CS;
     const size_t need = (CS + 2 * CS * (size_t)ng) * sizeof(unsigned);
     if (g_pl_bytes[dev] < need) {
         if (g_pl_ctr[dev]) {
             HCHK(hipStreamSynchronize(stream()));
+            const int rc = pl_check(); /* do not lose a pending error word */
             HCHK(hipFree(g_pl_ctr[dev]));
             g_pl_ctr[dev] = nullptr;
             g_pl_bytes[dev] = 0;
+            if (rc) return rc;
         }
         const size_t alloc = (need + 4095) & ~(size_t)4095;
         HCHK(hipMalloc((void **)&g_pl_ctr[dev], alloc));
+        HCHK(hipMemset(g_pl_ctr[dev], 0, alloc));
         g_pl_bytes[dev] = alloc;
         if (!g_pl_err_host[dev]) {
             HCHK(hipHostMalloc((void **)&g_pl_err_host[dev], 64, hipHostMallocDefault));
@@ -734,7 +743,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         }
     }
     unsigned *ctr = g_pl_ctr[dev];
-    HCHK(hipMemsetAsync(ctr, 0, need, stream()));
+    HCHK(hipMemsetAsync(ctr + CS, 0, need - CS * sizeof(unsigned), stream()));
     bxc::XArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)in;
@@ -750,6 +759,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     a.batch = (unsigned)batch;
     a.ng = (unsigned)ng;
     a.nsig = (unsigned)nsig;
+    bool sync_mode = false;
     {
         const char *e = getenv("HSFFT_BX_SLEEP");
         a.sleep = e ? (unsigned)atoi(e) : 1u;
@@ -761,6 +771,8 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
          * measured slower (c4 23.6-23.7 vs 24.3-24.5 GSamples/s with one acquire per wait) */
         e = getenv("HSFFT_BX_MERGE");
         a.merge = e ? (unsigned)atoi(e) & 1u : 0u;
+        e = getenv("HSFFT_BX_SYNC");
+        sync_mode = e && atoi(e);
     }
     static unsigned *s_dbg = nullptr;
     const char *dbgenv = getenv("HSFFT_BX_DEBUG");
@@ -769,13 +781,23 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, 4096 * 8 * sizeof(unsigned)));
         HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 8 * sizeof(unsigned), stream()));
         a.dbg = s_dbg;
+        sync_mode = true;
     }
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
-    HCHK(hipGetLastError());
+    void *kargs[] = {&a};
+    const hipError_t le = hipLaunchCooperativeKernel((const void *)fn, dim3((unsigned)grid), dim3(512), kargs,
+                                                     (unsigned)bxc::LDS_BYTES, stream());
+    if (le != hipSuccess) {
+        (void)hipGetLastError();
+        if (le == hipErrorCooperativeLaunchTooLarge) {
+            snprintf(g_err, sizeof g_err, "hsd_blue_xcd: cooperative launch of %d workgroups refused (not co-resident)", grid);
+            return 3; /* refused at launch: the caller runs the three-launch path */
+        }
+        return set_err(le, "hipLaunchCooperativeKernel(k_bxcd)");
+    }
     HCHK(hipMemcpyAsync(g_pl_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
+    if (!sync_mode) return 0;
     HCHK(hipStreamSynchronize(stream()));
     const unsigned err = *(volatile unsigned *)g_pl_err_host[dev];
-    *g_pl_err_host[dev] = 0;
     if (dbg) { /* mean us per row: P1, wait A, P2, wait B, P3 */
         static unsigned h[4096 * 8];
         HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
@@ -789,7 +811,10 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
                 grid, t[0] / grid, t[1] / rows / 100.0, t[6] / rows / 100.0, t[2] / rows / 100.0, t[3] / rows / 100.0,
                 t[7] / rows / 100.0, t[4] / rows / 100.0, t[5] / rows / 100.0);
     }
-    if (err) {
+    if (err) { /* sync mode: consume the word here (the caller re-runs the rows) */
+        *g_pl_err_host[dev] = 0;
+        HCHK(hipMemsetAsync(ctr + 8, 0, sizeof(unsigned), stream()));
+        HCHK(hipStreamSynchronize(stream()));
         snprintf(g_err, sizeof g_err, "hsd_blue_xcd: an in-launch wait timed out (error word %u)", err);
         return 2;
     }

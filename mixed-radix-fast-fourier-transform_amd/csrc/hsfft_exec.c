@@ -784,8 +784,8 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     return 0;
 }
 
-/* persistent Bluestein launches whose rows were re-run on the three-launch path (waits timed
- * out); read by hsfft_bluestein_fallbacks() */
+/* persistent Bluestein launches whose rows ran on the three-launch path instead (cooperative
+ * launch refused, or waits timed out in HSFFT_BX_SYNC=1 mode); hsfft_bluestein_fallbacks() */
 static long long g_blue_fallbacks;
 
 long long hsfft_bluestein_fallbacks(void) { return __atomic_load_n(&g_blue_fallbacks, __ATOMIC_RELAXED); }
@@ -808,9 +808,10 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
                      p0->radix[0] == 8 && !env_int("HSFFT_BLUE_NOFUSE", 0);
     /* one persistent launch per 65536 rows (hsfft_blue_xcd.h): groups of 64 workgroups carry
      * one row at a time through all three kernels, the intermediates stay on die
-     * (HSFFT_BLUE_XCD=0: three launches per chunk).  The launch is synchronous; if its waits
-     * timed out (its workgroups were not all resident), the rows from that launch on run on the
-     * three-launch path below. */
+     * (HSFFT_BLUE_XCD=0: three launches per chunk).  The launch is cooperative: if its grid
+     * cannot be co-resident the runtime refuses it and the rows run on the three-launch path
+     * below at once.  Asynchronous; in HSFFT_BX_SYNC=1 mode a launch whose waits timed out
+     * makes its rows run on the three-launch path as well.  Both count as fallbacks. */
     const int ng = env_int("HSFFT_BLUE_XCD", 8);
     long long done = 0;
     if (fuse && ng > 0) {
@@ -827,7 +828,7 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
             hs_seterr("bluestein persistent launch: %s", hsd_errstr());
             return HSFFT_ERR_DEVICE;
         }
-        if (rc == 2) __atomic_fetch_add(&g_blue_fallbacks, 1, __ATOMIC_RELAXED);
+        if (rc == 2 || rc == 3) __atomic_fetch_add(&g_blue_fallbacks, 1, __ATOMIC_RELAXED);
         if (done == batch) return 0;
     }
     if (done) {

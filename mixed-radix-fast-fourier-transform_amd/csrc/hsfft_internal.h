@@ -113,8 +113,10 @@ int mr_has_variant(const hsd_pass *p);
  * h+1 bins (hsfft_r2c_batched_compact) instead of the mirrored N */
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
                  long long B, int batch, int sgn, int compact);
-/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h), synchronous: 0 done, 1 not
- * applicable, 2 in-launch waits timed out (re-run the rows elsewhere), < 0 HIP error */
+/* Bluestein M = 2^18 in one persistent, cooperative launch (hsfft_blue_xcd.h), asynchronous
+ * (HSFFT_BX_SYNC=1: synchronous): 0 queued / done, 1 not applicable, 2 (sync mode) in-launch
+ * waits timed out, 3 cooperative launch refused (re-run the rows elsewhere in both), < 0 HIP
+ * error.  In async mode a timed-out wait is reported by the next hsd_sync. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
                  const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng);
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */

@@ -212,8 +212,8 @@ int hsd_blue_first(const void *in, long long idist, void *out, long long odist, 
     touch_rows_w(out, odist, odist, batch, 16);
     return 0;
 }
-/* null_bx_timeout = 1: the persistent Bluestein launch reports timed-out waits (return 2), so
- * the host's three-launch fallback runs */
+/* null_bx_timeout = 1: the persistent Bluestein launch reports timed-out waits (return 2, sync
+ * mode); 2: the cooperative launch is refused (return 3) -- the host's three-launch path runs */
 int null_bx_timeout;
 
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
@@ -223,7 +223,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     touch_rows_r(chirp, 0, nsig, 1, 16);
     touch_rows_r(hk, 0, 512 * 512, 1, 16);
     touch_rows_w(img, 0, (long long)(img_bytes / 16), 1, 16);
-    if (null_bx_timeout) return 2;
+    if (null_bx_timeout) return null_bx_timeout == 2 ? 3 : 2;
     touch_rows_w(out, odist, nsig, batch, 16);
     return 0;
 }

@@ -228,6 +228,10 @@ int main(void)
         CHECK(fb1 == fb0 + 6, "bluestein fallback count %lld", fb1 - fb0);
         run_c2c(99991, 2);
         CHECK(hsfft_bluestein_fallbacks() == fb1, "no fallback without a timeout");
+        null_bx_timeout = 2; /* the cooperative launch refused: same three-launch path */
+        run_c2c(99991, 3);
+        null_bx_timeout = 0;
+        CHECK(hsfft_bluestein_fallbacks() == fb1 + 6, "bluestein refusal count %lld", hsfft_bluestein_fallbacks() - fb1);
     }
 
     /* a caller edits the public fields between calls: the registry rebuilds its entry */

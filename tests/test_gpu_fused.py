@@ -168,6 +168,38 @@ def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
     assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
 
 
+@pytest.mark.parametrize("mode", ["refused", "sync"])
+def test_bluestein_persistent_launch_contract(mode, monkeypatch):
+    """The persistent Bluestein launch is cooperative (hipLaunchCooperativeKernel).  refused: 9
+    groups = 576 workgroups of which only 512 (two per CU) can be resident, so the runtime
+    refuses the launch and the rows run on the three-launch path at once -- results bit-exact,
+    one fallback counted per call, no ~1 s wait.  sync: HSFFT_BX_SYNC=1 (the synchronous form
+    with the automatic re-run) -- bit-exact, no fallback."""
+    import time
+    n, batch = 99991, 11
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "9" if mode == "refused" else "8")
+    if mode == "sync":
+        monkeypatch.setenv("HSFFT_BX_SYNC", "1")
+    x = T.complex_input(n, 0xC0C0, batch=batch).reshape(batch, n)
+    ref = _oracle(x, 1, ("coop", n, batch))
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    for it in range(2):
+        fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
+        dout.fill_zero()
+        t0 = time.perf_counter()
+        hsfft.exec_batched(p, din, dout, batch)
+        hsfft.synchronize()
+        dt = time.perf_counter() - t0
+        assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), ref), (mode, it)
+        assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0 + (1 if mode == "refused" else 0), mode
+        assert dt < 0.5, f"{mode}: {dt:.3f} s for {batch} rows (a refused launch must not wait)"
+    din.free()
+    dout.free()
+    p.close()
+
+
 @pytest.mark.parametrize("jitter", ["0", "2"])
 def test_bluestein_persistent_full_size_every_word(jitter, monkeypatch):
     """BASELINE config 4 at full size (99991 x 8192) through the persistent launch, compared on
