@@ -814,12 +814,20 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
         }
     }
     if ((mask & 2) && p->B > 1 && p->nst == 3 && p->radix[0] == 8 && p->A == 1 && p->B % 8 == 0) {
+        /* rows per workgroup: the tile's twiddles (64 KiB) are read once per TL rows (512 KiB
+         * of data at TL = 8: 12.5 % over-read; 16: 6 %, 32: 3 %) */
         const int t = env("HSFFT_PFB", 8);
-        *TL = t >= 8 ? 8 : t >= 4 ? 4 : 2;
+        *TL = t >= 32 ? 32 : t >= 16 ? 16 : t >= 8 ? 8 : t >= 4 ? 4 : 2;
         *G = 8;
         *threads = 512;
         *lds = (size_t)(512 * 8 + 504) * sizeof(double2);
-        return *TL == 8 ? b512_fn<8>(l->sgn, l->conj) : *TL == 4 ? b512_fn<4>(l->sgn, l->conj) : b512_fn<2>(l->sgn, l->conj);
+        switch (*TL) {
+        case 32: return b512_fn<32>(l->sgn, l->conj);
+        case 16: return b512_fn<16>(l->sgn, l->conj);
+        case 8: return b512_fn<8>(l->sgn, l->conj);
+        case 4: return b512_fn<4>(l->sgn, l->conj);
+        default: return b512_fn<2>(l->sgn, l->conj);
+        }
     }
     return nullptr;
 }
