@@ -672,6 +672,201 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
     }
 }
 
+/* ------------------------------------------------------------------ r2c split, two walks per CU
+ * k_r2c_walk2's split walk (whole-line stores through the one-lane shift and the carried entry)
+ * without its software pipeline, sized so that TWO workgroups share a CU (round 4): at most 128
+ * VGPRs and 80 KiB of LDS -- the split image (32 KiB), the hi tile's real parts (32 KiB) and the
+ * carry (16 KiB).  One tile buffer per thread; the stage-0 / stage-1 twiddle runs are read from
+ * the plan's table in global memory (L2 / Infinity-Cache hits) instead of an LDS copy, the
+ * stage-1 run issued behind stage 0.  A CU then overlaps one walk's loads and store drains with
+ * the other walk's stages, where the one-per-CU walk serialises them in its own phase order
+ * (every load issued after a store burst waits for that burst: vmcnt is in order). */
+constexpr int R2CW1_LDS = (512 * 8 + 1024) * 16;
+
+/* a run of 7 twiddles at table index idx (stage 0: B - 1 + 7q; stage 1: 8B - 1 + 7(q + B kl)) */
+__device__ __forceinline__ void tw_run(double2 (&w)[7], const double2 *tw, unsigned idx)
+{
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = ldg(tw, (idx + i) * 16u);
+}
+
+/* r8::redistribute_tw at an explicit 7-KiB wave region */
+__device__ __forceinline__ void redistribute_at(double2 (&w)[7], double2 *region)
+{
+    const unsigned lane = threadIdx.x & 63;
+    double2 *reg = region + (lane >> 3) * 56;
+#pragma unroll
+    for (int j = 0; j < 7; j++) reg[(lane & 7) + 8 * j] = w[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 7; i++) w[i] = reg[(lane & 7) * 7 + i];
+}
+
+/* one tile's row loads and its stage-0 run (registers) */
+__device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double2 (&w)[7], const double2 *row,
+                                        unsigned B, unsigned q0, const double2 *tw, unsigned tid)
+{
+    constexpr int TPG = 64;
+    const unsigned g = tid & 7, jt = tid >> 3;
+    const unsigned lane0 = (jt * B + q0 + g) * 16u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const double2 v = ldg(row + (size_t)i * TPG * B, lane0);
+        xr[i] = v.x;
+        xi[i] = v.y;
+    }
+    tw_run(w, tw, B - 1 + 7 * (q0 + g));
+}
+
+/* the tile's three stages with one twiddle run live at a time (<= 128 VGPRs with the hi tile's
+ * imaginary parts alongside): stage 0 with w, the stage-1 run loaded behind it, the coalesced
+ * stage-2 run loaded behind stage 1 and redistributed after the second exchange through the
+ * image's first half (waves 0-3, then 4-7: the second half may hold the hi tile's real parts);
+ * split exchanges through doubles [0, 4096) */
+template <int SGN>
+__device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], double2 (&w)[7], double2 *lds,
+                                          const double2 *tw, unsigned B, unsigned q0, unsigned tid0)
+{
+    constexpr int TPG = 64, P = 512, G = 8;
+    unsigned tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const unsigned g = tid & 7, jt = tid >> 3;
+    stage<8, SGN>(xr, xi, w, false);
+    tw_run(w, tw, 8 * B - 1 + 7 * (q0 + g + B * (jt & 7)));
+    r8::exchange<8, 1, 8, TPG, P, G, true>(xr, xi, lds, jt, g);
+    stage<8, SGN>(xr, xi, w, false);
+    {
+        r8::Args ta;
+        ta.tw = tw;
+        ta.B = B;
+        r8::load_tw_co<64>(w, ta, (int)jt, q0);
+    }
+    r8::exchange<8, 8, 8, TPG, P, G, true>(xr, xi, lds, jt, g); /* ends with a barrier: the image is free */
+    const unsigned wave = tid0 >> 6;
+    if (wave < 4) redistribute_at(w, lds + wave * 448);
+    __syncthreads();
+    if (wave >= 4) redistribute_at(w, lds + (wave - 4) * 448);
+    stage<8, SGN>(xr, xi, w, false);
+}
+
+template <int SGN>
+__global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
+{
+    constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    double2 *cry = lds + P * G;
+    double *ld = reinterpret_cast<double *>(lds); /* [0, 4096): split image / hi imag, [4096, 8192): hi real */
+    const unsigned blk = xcd_remap(blockIdx.x), nb = (unsigned)a.batch;
+    const unsigned b = a.tile_major ? blk % nb : blk / (W + 1), s = a.tile_major ? blk / nb : blk % (W + 1);
+    const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
+    const double2 *row = a.in + (long long)b * a.idist;
+    double2 *X = a.out + (long long)b * a.odist;
+    const double2 *w2t = a.saux;
+    if (s == W) { /* column 0 (k = u*B pairs with (P-u)*B), as k_r2c_fused (LDS: image + 8 KiB runs) */
+        double2 *ltw = lds + P * G;
+        const unsigned g = tid0 & 7, jt = tid0 >> 3;
+        double xr[8], xi[8];
+        double2 w2[7];
+        r2c_load(xr, xi, w2, row, B, 0, a.tw, lds, ltw, tid0);
+        r2c_stages<SGN, false>(xr, xi, w2, lds, ltw, tid0);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) lds[(jt + jj * TPG) * G + g] = make_double2(xr[jj], xi[jj]);
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B;
+            const double2 zk = make_double2(xr[jj], xi[jj]);
+            if (u == 0) {
+                X[0] = make_double2(zk.x + zk.y, 0.0);
+                X[h] = make_double2(zk.x - zk.y, 0.0);
+            } else {
+                const double2 zh = lds[(P - u) * G];
+                double re, im;
+                r8::r2c_pair(zk, zh, w2t[k], re, im);
+                X[k] = make_double2(re, im);
+                X[N - k] = make_double2(re, -im);
+            }
+        }
+        return;
+    }
+    /* walk segment, rotation and carry chains exactly as k_r2c_walk2 */
+    const unsigned j0 = s * T, j1 = min(j0 + T, B / 16), len = j1 - j0;
+    const unsigned nrot = a.tile_major >= 3 ? (unsigned)a.tile_major - 1 : 0u;
+    const unsigned o = len == 0 ? 0u
+                     : a.tile_major == 2 ? (b * 7u) % len
+                     : nrot ? ((b % nrot) * len) / nrot : 0u;
+#pragma unroll 1
+    for (unsigned jr = 0; jr < len; jr++) {
+        unsigned tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const unsigned g = tid & 7, jt = tid >> 3;
+        const unsigned j = j0 + (o + jr) % len;
+        const unsigned qlo = 8 * j + 1, qhi = B - 8 * j - 8;
+        double xr[8], xi[8], him[8];
+        double2 w[7];
+        /* ---- hi(j) */
+        w1_load(xr, xi, w, row, B, qhi, a.tw, tid);
+        __syncthreads(); /* the previous pairs phase has read the image */
+        w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qhi, tid);
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            ld[4096 + (jt + jj * TPG) * G + g] = xr[jj]; /* hi real parts wait in the image's second half */
+            him[jj] = xi[jj];
+        }
+        /* ---- lo(j) */
+        w1_load(xr, xi, w, row, B, qlo, a.tw, tid);
+        __syncthreads(); /* every wave's hi stage-2 twiddles are read back from the image */
+        w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qlo, tid);
+        __syncthreads();
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
+        __syncthreads();
+        /* ---- pairs: X[N-k], X[h-k] aligned; X[k], X[h+k] shifted one lane onto line [8j, 8j+8) */
+        const bool cstart = jr == 0 || j == j0;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, k = u * B + qlo + g, hk = h - k;
+            const unsigned sl = (P - 1 - u) * G + (7 - g);
+            const double2 zk = make_double2(xr[jj], xi[jj]), zh = make_double2(ld[4096 + sl], ld[sl]);
+            double re, im, re2, im2;
+            r8::r2c_pair(zk, zh, w2t[k], re, im);
+            r8::r2c_pair(zh, zk, w2t[hk], re2, im2);
+            X[N - k] = make_double2(re, -im);
+            X[hk] = make_double2(re2, im2);
+            const double2 va = grp_shift<-1>(make_double2(re, im)), vb = grp_shift<-1>(make_double2(re2, -im2));
+            const unsigned p = u * B + 8 * j + g;
+            if (g != 0) {
+                X[p] = va;
+                X[h + p] = vb;
+            } else {
+                if (!cstart) {
+                    X[p] = cry[u];
+                    X[h + p] = cry[512 + u];
+                } else if (jr != 0 && j1 < B / 16) { /* the first chain's carry: bin 8*j1 */
+                    X[u * B + 8 * j1] = cry[u];
+                    X[h + u * B + 8 * j1] = cry[512 + u];
+                }
+                cry[u] = va;
+                cry[512 + u] = vb;
+            }
+        }
+    }
+    const unsigned jend = o > 0 ? j0 + o : j1;
+    if (len > 0 && jend < B / 16 && (tid0 & 7) == 0) {
+        const unsigned jt = tid0 >> 3;
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned u = jt + jj * TPG, p = u * B + 8 * jend;
+            X[p] = cry[u];
+            X[h + p] = cry[512 + u];
+        }
+    }
+}
+
 inline int env(const char *name, int dflt);
 
 /* returns 1 if not applicable, 0 on launch, < 0 on error */
@@ -719,7 +914,11 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         static const wfn fws[2][2] = {{k_r2c_walk2<1, 0>, k_r2c_walk2<1, 1>}, {k_r2c_walk2<-1, 0>, k_r2c_walk2<-1, 1>}};
         wfn fw = fws[sgn == 1 ? 0 : 1][dbg ? 1 : 0];
 #endif
-        const int lds_bytes = R2CW2_LDS;
+        int lds_bytes = R2CW2_LDS;
+        if (env("HSFFT_R2C_WALK", 2) == 3) { /* two walks per CU (k_r2c_walk1) */
+            fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>;
+            lds_bytes = R2CW1_LDS;
+        }
         a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
         static unsigned *s_dbg = nullptr;
         static long long s_dbg_n = 0;

@@ -672,6 +672,28 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order,wt", [("9", "8"), ("0", "1"), ("0", "5"), ("0", "4096"), ("2", "5"), ("5", "16"),
+                                      ("1", "8")])
+@pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
+def test_r2c_walk1(n, sgn, order, wt, monkeypatch):
+    """pf::k_r2c_walk1 (HSFFT_R2C_WALK=3: the split walk sized for two workgroups per CU -- one
+    tile buffer, stage-0/1 twiddles from global memory, 80 KiB of LDS): walk lengths 1 (every
+    tile a walk's first), 5 (uneven walks), 4096 (one walk per row), the rotated and class
+    orders, segment-major order; bit-exact vs the oracle, odd batch, stale output buffer."""
+    monkeypatch.setenv("HSFFT_R2C_WALK", "3")
+    monkeypatch.setenv("HSFFT_R2C_WT", wt)
+    monkeypatch.setenv("HSFFT_R2C_ORDER", order)
+    x = T.real_input(n, 31, batch=3).reshape(3, n)
+    rp = hsfft.RealPlan(n, sgn)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(3 * n * 16)
+    hsfft.fill_complex(dout, 3 * n, 1)  # stale data: every bin must be written
+    hsfft.r2c_batched(rp, din, dout, 3)
+    y = dout.to_array(np.complex128).reshape(3, n)
+    assert T.bits_equal(y, T.oracle_r2c(x, sgn))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
