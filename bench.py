@@ -353,11 +353,20 @@ def place_output(din, dout, tries=3):
     output buffers.  The kept buffers and every probe rate are reported in the JSON line.
     Returns (din, dout, record)."""
     def rate(src, dst):
-        n = min(src.nbytes, dst.nbytes) // 16 * 16
-        ms = hsfft.bench_copy(src, dst, n, 2)
-        return round(2 * n * 2 / (ms / 1e3) / 1e9, 1)
+        """the slowest 4-GiB slice of dst: placement is decided per physical chunk, not per
+        buffer -- a 64 GiB output whose whole-buffer copy rate passed once held a slow half
+        that made every second c5 split launch 34 % slower (profiles/r04b_c5_walk_halves.txt)"""
+        sl = 4 << 30
+        n = min(src.nbytes, sl) // 16 * 16
+        worst = None
+        for off in range(0, dst.nbytes - 15, sl):
+            m = min(n, (dst.nbytes - off) // 16 * 16)
+            ms = hsfft.bench_copy(src, hsfft.DeviceView(dst, off), m, 2)
+            r = 2 * m * 2 / (ms / 1e3) / 1e9
+            worst = r if worst is None or r < worst else worst
+        return round(worst, 1)
 
-    rec = {"probe": "16-B stream copy into the output buffer, GB/s", "min_gbs": PLACE_MIN_GBS, "copy_gbs": []}
+    rec = {"probe": "16-B stream copy into every 4-GiB slice of the output buffer, slowest slice, GB/s", "min_gbs": PLACE_MIN_GBS, "copy_gbs": []}
     r = rate(din, dout)
     rec["copy_gbs"].append(r)
     if r >= PLACE_MIN_GBS:
@@ -416,7 +425,7 @@ def other_configs(steps=10, warmup=2, cpu=True, cpu_seconds=8.0):
             timed = lambda k: hsfft.time_batched(plan, bufs["in"], bufs["out"], batch, k)[0]  # noqa: E731
         else:
             plan = hsfft.RealPlan(n, 1)
-            chunk = min(batch, max(1, (64 << 30) // (n * 16)))
+            chunk = min(batch, max(1, (32 << 30) // (n * 16)))  # 512-row output chunks (32 GiB), as the headline
             bufs["in"], bufs["out"] = hsfft.DeviceBuffer(n * batch * 8), hsfft.DeviceBuffer(chunk * n * 16)
             fill = lambda: hsfft.fill_real(bufs["in"], n * batch, seed, 0)  # noqa: E731
 
@@ -610,8 +619,10 @@ def main():
         plan = hsfft.RealPlan(n, 1)
         # the whole per-GPU input stays resident (4096 x 2^22 x 8 B = 128 GiB); the mirrored
         # N-bin output (16 B per real sample) of all rows would not fit next to it in 288 GB,
-        # so the step writes it chunk by chunk into one output buffer a consumer would drain
-        chunk = min(batch, max(1, (64 << 30) // (n * 16)))
+        # so the step writes it chunk by chunk into one output buffer a consumer would drain:
+        # 512 rows (32 GiB) per call, the library's own chunk of the inner intermediate, so the
+        # placement check can afford up to three fresh output buffers next to the input
+        chunk = min(batch, max(1, (32 << 30) // (n * 16)))
         din = hsfft.DeviceBuffer(samples * 8)
         orow = (n // 2 + 1) if args.r2c_compact else n
         dout = hsfft.DeviceBuffer(chunk * orow * 16)

@@ -721,8 +721,8 @@ __device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double
 }
 
 /* the tile's three stages with one twiddle run live at a time (<= 128 VGPRs with the hi tile's
- * imaginary parts alongside): stage 0 with w, the stage-1 run loaded behind it, the coalesced
- * stage-2 run loaded behind stage 1 and redistributed after the second exchange through the
+ * imaginary parts alongside): stage 0 with w, the stage-1 run loaded after the first exchange,
+ * the coalesced stage-2 run after the second and redistributed through the
  * image's first half (waves 0-3, then 4-7: the second half may hold the hi tile's real parts);
  * split exchanges through doubles [0, 4096) */
 template <int SGN>
@@ -734,16 +734,17 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
     asm volatile("" : "+v"(tid));
     const unsigned g = tid & 7, jt = tid >> 3;
     stage<8, SGN>(xr, xi, w, false);
-    tw_run(w, tw, 8 * B - 1 + 7 * (q0 + g + B * (jt & 7)));
     r8::exchange<8, 1, 8, TPG, P, G, true>(xr, xi, lds, jt, g);
+    tw_run(w, tw, 8 * B - 1 + 7 * (q0 + g + B * (jt & 7))); /* after the exchange: issued earlier,
+                                                                * its 28 VGPRs spill (19 dwords) */
     stage<8, SGN>(xr, xi, w, false);
+    r8::exchange<8, 8, 8, TPG, P, G, true>(xr, xi, lds, jt, g); /* ends with a barrier: the image is free */
     {
         r8::Args ta;
         ta.tw = tw;
         ta.B = B;
         r8::load_tw_co<64>(w, ta, (int)jt, q0);
     }
-    r8::exchange<8, 8, 8, TPG, P, G, true>(xr, xi, lds, jt, g); /* ends with a barrier: the image is free */
     const unsigned wave = tid0 >> 6;
     if (wave < 4) redistribute_at(w, lds + wave * 448);
     __syncthreads();
