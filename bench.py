@@ -397,6 +397,23 @@ def place_output(din, dout, tries=3):
     return din, best, rec
 
 
+def probe_placement(din, dout):
+    """Diagnostic only (the buffers are not changed): the copy rate into every 4-GiB slice of the
+    output buffer.  Round 3 selected buffers by this kind of probe; round 4 found it does not
+    predict the r2c split's time (a first allocation whose slices all copied at 5.46-5.74 TB/s ran
+    c5 at 105.8 GSamples/s, the re-allocated 'best' one at 87.6: profiles/r04c_*), so the bench
+    line now times the buffers as first allocated and only reports the probe."""
+    sl = 4 << 30
+    n = min(din.nbytes, sl) // 16 * 16
+    rates = []
+    for off in range(0, dout.nbytes - 15, sl):
+        m = min(n, (dout.nbytes - off) // 16 * 16)
+        ms = hsfft.bench_copy(din, hsfft.DeviceView(dout, off), m, 2)
+        rates.append(round(2 * m * 2 / (ms / 1e3) / 1e9, 1))
+    return {"probe": "16-B stream copy into each 4-GiB slice of the output buffer, GB/s (diagnostic; buffers "
+                     "kept as first allocated)", "slice_copy_gbs": rates}
+
+
 def other_configs(steps=10, warmup=2, cpu=True, cpu_seconds=8.0):
     """The other BASELINE configs, each at its full per-GPU workload, timed in the same run as
     the headline (one rank): `steps` steps between HIP events on the library stream after
@@ -451,11 +468,8 @@ def other_configs(steps=10, warmup=2, cpu=True, cpu_seconds=8.0):
             hsfft.synchronize()
             return (time.perf_counter() - t0) / steps * 1e3, timed(steps) / steps
 
-        # the buffers as first allocated (what a caller's plain hipMalloc gets) ...
-        fill()
-        wall_first, ev_first = measure()
-        # ... then the placement-checked buffers (bench.py place_output): value is this one
-        bufs["in"], bufs["out"], place = place_output(bufs["in"], bufs["out"])
+        # the buffers as first allocated (what a caller's plain hipMalloc gets): no selection
+        place = probe_placement(bufs["in"], bufs["out"])
         fill()
         wall_ms, ev_ms = measure()
         din, dout = bufs["in"], bufs["out"]
@@ -464,10 +478,7 @@ def other_configs(steps=10, warmup=2, cpu=True, cpu_seconds=8.0):
         ach = alg / (ev_ms / 1e3) / 1e9
         ent = traffic_entry(name)
         out[name] = {"value": round(n * batch / (ev_ms / 1e3) / 1e9, 3), "unit": "GSamples/s",
-                     "value_basis": "placement-checked buffers (place_output); first_allocation: the same "
-                                    "steps on the buffers as first allocated, same run",
-                     "first_allocation": {"value": round(n * batch / (ev_first / 1e3) / 1e9, 3),
-                                          "ms_per_step": round(ev_first, 3), "wall_ms_per_step": round(wall_first, 3)},
+                     "value_basis": "buffers as first allocated (plain hipMalloc, no placement selection)",
                      "ms_per_step": round(ev_ms, 3), "wall_ms_per_step": round(wall_ms, 3), "steps": steps,
                      "warmup": warmup, "frac": round(ach / HBM_PEAK_GBS, 4),
                      "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -654,16 +665,10 @@ def main():
         comm.barrier()
         return comm.max(time.perf_counter() - t0)
 
-    first_alloc = None
+    # the buffers as first allocated -- what a caller's plain hipMalloc gets; no placement
+    # selection (probe_placement only reports the output buffer's slice copy rates)
     if fill is not None:
-        # the buffers as first allocated -- what a caller's plain hipMalloc gets -- timed first;
-        # then the output placement is checked (place_output: swap or re-allocate a slow-write
-        # output buffer), the input regenerated, and the headline steps timed on the result
-        fill()
-        wall1 = timed_steps()
-        first_alloc = {"value": round(samples * ws / (wall1 / args.steps) / 1e9, 3),
-                       "ms_per_step": round(wall1 / args.steps * 1e3, 4)}
-        din, dout, place = place_output(din, dout)
+        place = probe_placement(din, dout)
         fill()
         hsfft.synchronize()
     wall = timed_steps()
@@ -705,11 +710,7 @@ def main():
     }
     if place:
         out["placement"] = place
-    if first_alloc:
-        out["value_basis"] = ("placement-checked buffers: the output buffer's copy rate probed and a slow-write "
-                              "placement swapped / re-allocated (place_output); first_allocation = the same "
-                              "warmup + steps on the buffers as first allocated, earlier in this run")
-        out["first_allocation"] = first_alloc
+    out["value_basis"] = "buffers as first allocated (plain hipMalloc, no placement selection)"
     # the transform as a whole: algorithmic bytes of the step / event-timed step time
     ach = samples * bytes_per_sample / (ev_step_ms / 1e3) / 1e9
     ent = traffic_entry(args.config)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-4 GPU session D: c5 split walk1 (two per CU) sweep of walk length / order against walk2 on
+# one set of buffers (two independent allocations), then the default bench line (first
+# allocations, no placement selection)
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+V='HSFFT_R2C_WALK=2 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=8 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=16 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=32 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=16;HSFFT_R2C_ORDER=0 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=32;HSFFT_R2C_ORDER=0 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=16;HSFFT_R2C_ORDER=2 HSFFT_R2C_WALK=3;HSFFT_R2C_WT=64;HSFFT_R2C_ORDER=0'
+for a in 1 2; do
+timeout -k 10 400 python -u tools/ab_env.py --config c5 --values $V --rounds 4 --iters 2 > gpurun_out/d_c5_walk_$a.log 2>&1; rc=$?; grep -E "placement|median" gpurun_out/d_c5_walk_$a.log; [ $rc = 0 ] || exit $rc
+done
+timeout -k 10 600 python -u bench.py > gpurun_out/d_bench.log 2>&1; rc=$?; tail -c 600 gpurun_out/d_bench.log; exit $rc
