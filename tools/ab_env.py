@@ -10,7 +10,8 @@ its knobs per launch, so setting os.environ between calls switches the variant.
 
 A value is either one setting of --var ("unset" removes it) or a ';'-separated list of VAR=VAL
 assignments; every variable named anywhere is removed before a variant's own are applied.  The
-output buffer is placement-checked first (bench.place_output).
+output buffer is kept as first allocated (bench.probe_placement reports its slice copy rates;
+--place selects it by the round-3 probe, bench.place_output, instead).
 """
 import argparse
 import os
@@ -40,6 +41,7 @@ def main():
                     help="comma-separated values of --var ('unset' removes it) or VAR=VAL;VAR=VAL sets")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--place", action="store_true", help="select the output buffer by bench.place_output")
     a = ap.parse_args()
     n, rows, real = CONFIGS[a.config]
     hsfft.lib().hsfft_set_device(0)
@@ -47,13 +49,13 @@ def main():
         p = hsfft.RealPlan(n, 1)
         din = hsfft.DeviceBuffer(rows * n * 8)
         dout = hsfft.DeviceBuffer(rows * n * 16)
-        din, dout, rec = bench.place_output(din, dout)
+        din, dout, rec = bench.place_output(din, dout) if a.place else (din, dout, bench.probe_placement(din, dout))
         hsfft.fill_real(din, rows * n, 0x55)
     else:
         p = hsfft.Plan(n, 1)
         din = hsfft.DeviceBuffer(rows * n * 16)
         dout = hsfft.DeviceBuffer(rows * n * 16)
-        din, dout, rec = bench.place_output(din, dout)
+        din, dout, rec = bench.place_output(din, dout) if a.place else (din, dout, bench.probe_placement(din, dout))
         hsfft.fill_complex(din, rows * n, 0x55)
     print("placement", rec, flush=True)
     vals = [v for arg in a.values for v in (arg.split(",") if "=" not in arg else [arg])]
