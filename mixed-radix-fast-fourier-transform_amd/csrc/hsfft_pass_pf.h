@@ -123,7 +123,7 @@ __device__ __forceinline__ void tw8_lds(double2 (&w)[7], const double2 *ltw, uns
 }
 
 /* stages + exchanges + store of one first-pass tile held in xr/xi; ocol = output column */
-template <int R0, int N8, int G, int SGN, bool CONJ, bool TWG = false>
+template <int R0, int N8, int G, int SGN, bool CONJ, bool TWG = false, bool NTS = false>
 __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], double2 *lds, const double2 *ltw,
                                            double2 *orow, unsigned m, unsigned jt, unsigned g,
                                            const double2 *gtw = nullptr)
@@ -153,7 +153,10 @@ __device__ __forceinline__ void first_body(double (&xr)[8], double (&xi)[8], dou
     /* last stage: output u = jt + jj*LL of the column, written to [m][u] */
     constexpr int LL = S::Lloc(S::NST - 1);
 #pragma unroll
-    for (int jj = 0; jj < 8; jj++) stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
+    for (int jj = 0; jj < 8; jj++) {
+        if constexpr (NTS) stg_nt(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
+        else stg(orow + jj * LL, (m * P + jt) * 16u, make_double2(xr[jj], xi[jj]));
+    }
 }
 
 /* ------------------------------------------------------------------ first pass, paired loads
@@ -178,7 +181,7 @@ __device__ __forceinline__ double pair_swap(double v)
     return r;
 }
 
-template <int R0, int N8, int G, int SGN, bool CONJ>
+template <int R0, int N8, int G, int SGN, bool CONJ, bool NTS = false>
 __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
 {
     using S = Shape<R0, N8>;
@@ -231,8 +234,8 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), 4) void k_firstq(Args a)
             yr[k] = pair_swap<G>(oth.x);
             yi[k] = pair_swap<G>(oth.y);
         }
-        first_body<R0, N8, G, SGN, CONJ, TWG>(xr, xi, lds, ltw, orow, m0 + h, jt, h, a.tw);
-        first_body<R0, N8, G, SGN, CONJ, TWG>(yr, yi, lds, ltw, orow, m0 + G + h, jt, h, a.tw);
+        first_body<R0, N8, G, SGN, CONJ, TWG, NTS>(xr, xi, lds, ltw, orow, m0 + h, jt, h, a.tw);
+        first_body<R0, N8, G, SGN, CONJ, TWG, NTS>(yr, yi, lds, ltw, orow, m0 + G + h, jt, h, a.tw);
     }
 }
 
@@ -895,8 +898,15 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
      * slower: workgroups that read the same lines at the same time contend); plain
      * segment-major (1) 88.7-90.8 elsewhere; HSFFT_R2C_WALK=0 (and the compact layout):
      * k_r2c_fused */
-    if (!compact && env("HSFFT_R2C_WALK", 2) != 0) {
-        const long long T = env("HSFFT_R2C_WT", 8) > 0 ? env("HSFFT_R2C_WT", 8) : 8, W = (B / 16 + T - 1) / T;
+    /* default (round 4): k_r2c_walk1 -- two walks per CU, walks of 32 tile pairs, 8 rotation
+     * classes; in-process A/B per 512 rows against k_r2c_walk2 (walks of 8): 20.40 vs 20.31 ms on a
+     * fast-write allocation, 20.97 vs 22.20 on a medium one, 22.25-23.60 vs 24.23-25.77 on three
+     * slow ones (profiles/r04d-f_*).  HSFFT_R2C_WALK=2: walk2; 0: k_r2c_fused */
+    const int walk = env("HSFFT_R2C_WALK", 3);
+    if (!compact && walk != 0) {
+        const int wt_dflt = walk == 3 ? 32 : 8;
+        const long long T = env("HSFFT_R2C_WT", wt_dflt) > 0 ? env("HSFFT_R2C_WT", wt_dflt) : wt_dflt,
+                        W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
         /* HSFFT_R2C_NT (measurement): bit 0 non-temporal data loads, bit 1 non-temporal stores */
@@ -916,7 +926,7 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         wfn fw = fws[sgn == 1 ? 0 : 1][dbg ? 1 : 0];
 #endif
         int lds_bytes = R2CW2_LDS;
-        if (env("HSFFT_R2C_WALK", 2) == 3) { /* two walks per CU (k_r2c_walk1) */
+        if (walk == 3 && !dbg) { /* two walks per CU (k_r2c_walk1); the phase trace is walk2's */
             fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>;
             lds_bytes = R2CW1_LDS;
         }
@@ -1009,6 +1019,11 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = q;
             *threads = 512;
             *lds = (size_t)4096 * sizeof(double) + 511 * sizeof(double2);
+            /* HSFFT_PFA_NT=1 (measurement): non-temporal output stores, so the 8 MiB of output an
+             * XCD's 64 workgroups write per column group do not evict the input lines their
+             * neighbours still have to read (pass A fetches 1.7x its input) */
+            if (env("HSFFT_PFA_NT", 0) && !l->conj)
+                return l->sgn == 1 ? k_firstq<8, 3, 1, 1, false, true> : k_firstq<8, 3, 1, -1, false, true>;
             if (l->sgn == 1) return l->conj ? k_firstq<8, 3, 1, 1, true> : k_firstq<8, 3, 1, 1, false>;
             return l->conj ? k_firstq<8, 3, 1, -1, true> : k_firstq<8, 3, 1, -1, false>;
         }

@@ -97,6 +97,24 @@ def test_paired_load_first_pass_2p21(pfp, monkeypatch):
         p.close()
 
 
+def test_paired_load_first_pass_2p21_nt_stores(monkeypatch):
+    """the same pass with non-temporal output stores (HSFFT_PFA_NT=1): bit-exact, both signs"""
+    monkeypatch.setenv("HSFFT_PFA_NT", "1")
+    n = 1 << 21
+    x = T.complex_input(n, 0x2121, batch=3).reshape(3, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, 3)
+        hsfft.synchronize()
+        y = dout.to_array(np.complex128).reshape(3, n)
+        assert T.bits_equal(y, _oracle(x, sgn, "2p21")), sgn
+        din.free()
+        dout.free()
+        p.close()
+
+
 @pytest.mark.parametrize("n,batch,chunk_mb", [(1 << 20, 7, "32"), (4096, 33, "1"), (12600, 5, "1"), (99991, 3, "2")])
 def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
     """hsfft_exec_batched_host (host rows streamed through HBM in chunks, upload / transform /

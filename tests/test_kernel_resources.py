@@ -23,12 +23,15 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 #  that the register allocation allows -- the occupancy each kernel's launch geometry assumes)
 BUDGETS = [
     # 2^20 pass A (c2): 512 threads, 2 workgroups per CU need 4 waves per SIMD
-    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]EE", 0, 128, 4),
+    (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]ELb0EE", 0, 128, 4),
     # 2^20 pass B (c2)
     (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]EE", 0, 112, 4),
     # 2^21 pass A (c5)
-    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]EE", 0, 128, 4),
-    # r2c split walk (c5): one 512-thread workgroup per CU with up to 256 VGPRs
+    (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]ELb[01]EE", 0, 128, 4),
+    # r2c split walk (c5, default since round 4): two 512-thread workgroups per CU, 128 VGPRs;
+    # one dword of spill (reloaded where the stage-2 twiddles are waited for anyway)
+    (r"^_ZN2pf11k_r2c_walk1ILin?1E", 1, 128, 4),
+    # the one-per-CU walk (HSFFT_R2C_WALK=2): up to 256 VGPRs
     (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0, 256, 2),
     # 12600 row kernel (c3): one 512-thread workgroup per CU
     (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1E", 0, 256, 2),
