@@ -1005,6 +1005,8 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = env("HSFFT_PFQ", 4) > 0 ? env("HSFFT_PFQ", 4) : 4;
             *threads = 512;
             *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
+            if (env("HSFFT_PFA_NT", 0) & 2 && !l->conj) /* measurement: non-temporal output stores */
+                return l->sgn == 1 ? k_firstq<4, 3, 2, 1, false, true> : k_firstq<4, 3, 2, -1, false, true>;
             if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 2, 1, true> : k_firstq<4, 3, 2, 1, false>;
             return l->conj ? k_firstq<4, 3, 2, -1, true> : k_firstq<4, 3, 2, -1, false>;
         }
@@ -1019,10 +1021,11 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = q;
             *threads = 512;
             *lds = (size_t)4096 * sizeof(double) + 511 * sizeof(double2);
-            /* HSFFT_PFA_NT=1 (measurement): non-temporal output stores, so the 8 MiB of output an
-             * XCD's 64 workgroups write per column group do not evict the input lines their
-             * neighbours still have to read (pass A fetches 1.7x its input) */
-            if (env("HSFFT_PFA_NT", 0) && !l->conj)
+            /* non-temporal output stores (HSFFT_PFA_NT bit 0, default on): the 8 MiB of output an
+             * XCD's 64 workgroups write per column group no longer evict the input lines their
+             * neighbours still have to read -- FETCH -17 %, pass A 7.29 -> 7.01 ms per 512 rows,
+             * c5 21.44 -> 21.12 ms (profiles/r04g_*) */
+            if ((env("HSFFT_PFA_NT", 1) & 1) && !l->conj)
                 return l->sgn == 1 ? k_firstq<8, 3, 1, 1, false, true> : k_firstq<8, 3, 1, -1, false, true>;
             if (l->sgn == 1) return l->conj ? k_firstq<8, 3, 1, 1, true> : k_firstq<8, 3, 1, 1, false>;
             return l->conj ? k_firstq<8, 3, 1, -1, true> : k_firstq<8, 3, 1, -1, false>;

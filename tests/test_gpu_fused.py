@@ -66,6 +66,16 @@ def test_pipelined_passes_bit_exact(pf, monkeypatch):
         assert T.bits_equal(_run(x, sgn), _oracle(x, sgn, "b3")), (pf, sgn)
 
 
+@pytest.mark.parametrize("nt", ["0", "2"])
+def test_first_pass_2p20_nt_stores(nt, monkeypatch):
+    """2^20's pass A (k_firstq<4,3,2>) with non-temporal output stores (HSFFT_PFA_NT bit 1):
+    bit-exact, both signs"""
+    monkeypatch.setenv("HSFFT_PFA_NT", nt)
+    x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
+    for sgn in (1, -1):
+        assert T.bits_equal(_run(x, sgn), _oracle(x, sgn, "b3")), (nt, sgn)
+
+
 @pytest.mark.parametrize("q", ["1", "2", "3"])
 def test_quad_load_first_pass(q, monkeypatch):
     """pf::k_firstq (64-B column loads, DPP quad swap): bit-exact, both signs, with a
@@ -97,9 +107,11 @@ def test_paired_load_first_pass_2p21(pfp, monkeypatch):
         p.close()
 
 
-def test_paired_load_first_pass_2p21_nt_stores(monkeypatch):
-    """the same pass with non-temporal output stores (HSFFT_PFA_NT=1): bit-exact, both signs"""
-    monkeypatch.setenv("HSFFT_PFA_NT", "1")
+@pytest.mark.parametrize("nt", ["0", "1"])
+def test_paired_load_first_pass_2p21_nt_stores(nt, monkeypatch):
+    """the same pass with plain / non-temporal (default) output stores (HSFFT_PFA_NT bit 0):
+    bit-exact, both signs"""
+    monkeypatch.setenv("HSFFT_PFA_NT", nt)
     n = 1 << 21
     x = T.complex_input(n, 0x2121, batch=3).reshape(3, n)
     for sgn in (1, -1):
