@@ -555,6 +555,109 @@ __device__ __forceinline__ void xchg1_ab_std(double *x, double *ld, int jt)
     }
 }
 
+/* k_row2 F45: the last two stages ([7, 8] at L = P/56) fused with TWO threads per group instead of
+ * an exchange through the split image.  Group g (< G45 = P/56) is the 8 stage-4 butterflies
+ * (ml = 0..7, kloc = g) and the 7 stage-5 butterflies kloc5 = g + jj*G45 (jj < 7): stage-5
+ * butterfly jj takes output jj of every stage-4 butterfly of the group.  Thread pair (2g, 2g+1)
+ * of one wave holds it: thread A (even) the stage-4 butterflies ml = 0..3, thread B (odd) ml =
+ * 4..7; after stage 4 they swap, through one DPP lane swap per dword, the 16 outputs A's stage-5
+ * butterflies (jj = 0..3) need from B and the 12 B's (jj = 4..6) need from A -- no LDS, no block
+ * barrier.  Same twiddles (stage 4 from the transposed LDS copy, stage 5 from global), skips and
+ * operand order as rstage, so the results are bit-identical. */
+__device__ __forceinline__ double lane_swap(double v)
+{
+    int2 u;
+    __builtin_memcpy(&u, &v, 8);
+    u.x = __builtin_amdgcn_mov_dpp(u.x, 0xB1, 0xF, 0xF, false); /* quad_perm [1,0,3,2] */
+    u.y = __builtin_amdgcn_mov_dpp(u.y, 0xB1, 0xF, 0xF, false);
+    double r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+}
+
+/* exchange fused_ab's outputs (as xchg1_ab_std writes them) into F45's stage-4 inputs: thread
+ * (g, h) reads butterflies ml = 4h + c (c < 4) at kloc = g, point i at (ml + 8i)*G45 + g */
+template <int RA, int RB, int L, int P, int TPG>
+__device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
+{
+    constexpr int Q = RA * RB, NG2 = P / Q, NGT = cdiv(NG2, TPG), LN = L * Q, G45 = P / 56;
+    static_assert(LN == G45, "F45 follows F23 at L = P / 56");
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NGT; c++) {
+        const int g = c * TPG + jt;
+        if (NGT * TPG != NG2 && g >= NG2) continue;
+        const int mlp = g / L, kloc = g % L;
+#pragma unroll
+        for (int jj = 0; jj < RA; jj++)
+#pragma unroll
+            for (int jq = 0; jq < RB; jq++) ld[mlp * LN + kloc + jj * L + jq * L * RA] = x[c * Q + jj * RB + jq];
+    }
+    __syncthreads();
+    const int h = jt & 1;
+    int g = jt >> 1;
+    if (g >= G45) g = G45 - 1; /* idle threads read a valid group */
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int i = 0; i < 7; i++) x[c * 7 + i] = ld[(4 * h + c + 8 * i) * G45 + g];
+}
+
+/* stages 4 (radix 7) and 5 (radix 8) of the pair's group, then the row's stores */
+template <int P, int TPG, bool CONJ>
+__device__ __forceinline__ void fused45_pair(double *xr, double *xi, const double2 *ltw, const double2 *tw,
+                                             double2 *out, int jt, int sgn)
+{
+    constexpr int G45 = P / 56, L4 = G45, L5 = 7 * G45;
+    const int h = jt & 1, g0 = jt >> 1;
+    const bool live = g0 < G45;
+    const unsigned g = live ? (unsigned)g0 : (unsigned)(G45 - 1);
+    /* stage 4: butterflies ml = 4h + c at k = g (radix 7 skips k == 0) */
+    {
+        const double2 *twa = ltw + (L4 - 1);
+        double2 t[6];
+#pragma unroll
+        for (int i = 1; i < 7; i++) t[i - 1] = twa[(i - 1) * L4 + g];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            if (g != 0) {
+#pragma unroll
+                for (int i = 1; i < 7; i++) hsb::twmul(xr[c * 7 + i], xi[c * 7 + i], t[i - 1].x, CONJ ? -t[i - 1].y : t[i - 1].y);
+            }
+            hsb::bfly<7>(&xr[c * 7], &xi[c * 7], sgn, false);
+        }
+    }
+    /* stage 5, one butterfly per step d: this thread's is jj = d (A) or 4 + d (B, d < 3; B's
+     * d = 3 is idle), k = g + jj*G45.  Per step the pair swaps 4 values: A sends output 4 + d of
+     * its butterflies (B's inputs 0..3), B sends output d of its butterflies (A's inputs 4..7) */
+    const double2 *twb = tw + (L5 - 1);
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int jj = h ? 4 + d : d, da = d < 3 ? 4 + d : 6;
+        double zr[8], zi[8];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const double sr = lane_swap(h ? xr[i * 7 + d] : xr[i * 7 + da]);
+            const double si = lane_swap(h ? xi[i * 7 + d] : xi[i * 7 + da]);
+            zr[i] = h ? sr : xr[i * 7 + d];
+            zi[i] = h ? si : xi[i * 7 + d];
+            zr[4 + i] = h ? xr[i * 7 + da] : sr;
+            zi[4 + i] = h ? xi[i * 7 + da] : si;
+        }
+        const unsigned k = g + (unsigned)(h && d == 3 ? 0 : jj) * G45; /* B's d = 3 is idle: a valid k */
+#pragma unroll
+        for (int i = 1; i < 8; i++) {
+            const double2 t = pf::ldg(twb, (7 * k + i - 1) * 16u);
+            hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
+        }
+        hsb::bfly<8>(zr, zi, sgn, false);
+        if (live && (h == 0 || d < 3)) {
+#pragma unroll
+            for (int j5 = 0; j5 < 8; j5++) pf::stg(out, (k + (unsigned)j5 * L5) * 16u, make_double2(zr[j5], zi[j5]));
+        }
+    }
+}
+
 /* fused01 for a row whose points [0, 2*P/R0) were prefetched into `pre` by LDS-DMA (k_row2
  * PRE): the remaining leaf inputs (i = R0-1) are loaded from global first, then one barrier
  * behind every wave's vmcnt(0) (all LDS-DMA has landed), then the prefetched inputs are read
@@ -640,9 +743,10 @@ constexpr int ROW_PRE_PTS = 8448;
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false>
+          bool F23 = false, bool F45 = false>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
+    static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
     static_assert(PF == 0 || (F01 && !PRE), "PF prefetches fused01's first groups");
     static_assert(!F23 || (F01 && !PRE), "F23 follows fused01");
     using LS = List6<R0, R1, R2, R3, R4, R5>;
@@ -730,6 +834,17 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             xchg_split<R0, 1, R1, P, TPG>(xr, xi, img, jt);
             rstage<R1, LS::Lloc(1), P, TPG, false, CONJ, true>(xr, xi, ltw + (LS::Lloc(1) - 1), jt, sgn);
             xchg_split<R1, LS::Lloc(1), R2, P, TPG>(xr, xi, img, jt);
+        }
+        if constexpr (F45) { /* stages 2-3 fused, then 4-5 fused over thread pairs: two exchanges */
+            fused_ab<R2, R3, LS::Lloc(2), P, TPG, CONJ>(xr, xi, ltw, jt, sgn);
+            mark(a, tp, 2);
+            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
+            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
+            mark(a, tp, 3);
+            fused45_pair<P, TPG, CONJ>(xr, xi, ltw, a.tw, out, jt, sgn);
+            mark(a, tp, 6);
+            if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + 7] += 1;
+            continue;
         }
         if constexpr (F23) { /* stages 2 and 3 fused in registers: one exchange fewer */
             fused_ab<R2, R3, LS::Lloc(2), P, TPG, CONJ>(xr, xi, ltw, jt, sgn);
@@ -882,10 +997,17 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * fused in registers as stages 0 and 1 are -- three exchanges per row instead of four */
         const char *e23 = getenv("HSFFT_ROW_F23");
         const bool f23 = e23 ? atoi(e23) != 0 : true;
-        const kfn fn = f23 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true>
-                                     : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true>)
-                           : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
-                                     : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>);
+        /* F45 (HSFFT_ROW_F45): stages 4 and 5 ([7,8], 225 groups of 56 points) fused over thread
+         * pairs (DPP lane swaps): two exchanges per row */
+        const char *e45 = getenv("HSFFT_ROW_F45");
+        const bool f45 = f23 && e45 && atoi(e45) != 0;
+        kfn fn = f23 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true>
+                               : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true>)
+                     : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
+                               : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>);
+        if (f45)
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true>;
         const int threads = 512;
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));

@@ -694,7 +694,7 @@ def test_r2c_walk1(n, sgn, order, wt, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}])
+@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "1"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -704,7 +704,7 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     the fused first stages are read right after the per-workgroup LDS copy).  Schedules:
     mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, the next row's
     first input group prefetched into registers), the same without the stage 2-3 fusion, and
-    the two mixed-radix passes."""
+    the two mixed-radix passes, and stages 4-5 fused over thread pairs (F45)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600
