@@ -707,9 +707,9 @@ __device__ __forceinline__ void redistribute_at(double2 (&w)[7], double2 *region
     for (int i = 0; i < 7; i++) w[i] = reg[(lane & 7) * 7 + i];
 }
 
-/* one tile's row loads and its stage-0 run (registers) */
-__device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double2 (&w)[7], const double2 *row,
-                                        unsigned B, unsigned q0, const double2 *tw, unsigned tid)
+/* one tile's row loads */
+__device__ __forceinline__ void w1_rows(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned B, unsigned q0,
+                                        unsigned tid)
 {
     constexpr int TPG = 64;
     const unsigned g = tid & 7, jt = tid >> 3;
@@ -720,7 +720,14 @@ __device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double
         xr[i] = v.x;
         xi[i] = v.y;
     }
-    tw_run(w, tw, B - 1 + 7 * (q0 + g));
+}
+
+/* one tile's row loads and its stage-0 run (registers) */
+__device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double2 (&w)[7], const double2 *row,
+                                        unsigned B, unsigned q0, const double2 *tw, unsigned tid)
+{
+    w1_rows(xr, xi, row, B, q0, tid);
+    tw_run(w, tw, B - 1 + 7 * (q0 + (tid & 7)));
 }
 
 /* the tile's three stages with one twiddle run live at a time (<= 128 VGPRs with the hi tile's
@@ -755,7 +762,9 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
     stage<8, SGN>(xr, xi, w, false);
 }
 
-template <int SGN>
+/* PFH: the next tile's hi rows are loaded at the start of this tile's pairs phase, i.e. before
+ * its store burst, so waiting for them does not wait for the stores (vmcnt is in order) */
+template <int SGN, bool PFH = false>
 __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -803,6 +812,9 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
     const unsigned o = len == 0 ? 0u
                      : a.tile_major == 2 ? (b * 7u) % len
                      : nrot ? ((b % nrot) * len) / nrot : 0u;
+    double pr[8], pi[8]; /* PFH: the next hi tile's rows */
+    if constexpr (PFH)
+        if (len > 0) w1_rows(pr, pi, row, B, B - 8 * (j0 + o) - 8, tid0);
 #pragma unroll 1
     for (unsigned jr = 0; jr < len; jr++) {
         unsigned tid = tid0;
@@ -813,7 +825,16 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
         double xr[8], xi[8], him[8];
         double2 w[7];
         /* ---- hi(j) */
-        w1_load(xr, xi, w, row, B, qhi, a.tw, tid);
+        if constexpr (PFH) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                xr[i] = pr[i];
+                xi[i] = pi[i];
+            }
+            tw_run(w, a.tw, B - 1 + 7 * (qhi + g));
+        } else {
+            w1_load(xr, xi, w, row, B, qhi, a.tw, tid);
+        }
         __syncthreads(); /* the previous pairs phase has read the image */
         w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qhi, tid);
 #pragma unroll
@@ -830,6 +851,10 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
         for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
         __syncthreads();
         /* ---- pairs: X[N-k], X[h-k] aligned; X[k], X[h+k] shifted one lane onto line [8j, 8j+8) */
+        if constexpr (PFH) { /* unconditional: the last tile reloads itself */
+            const unsigned jn = jr + 1 < len ? j0 + (o + jr + 1) % len : j;
+            w1_rows(pr, pi, row, B, B - 8 * jn - 8, tid);
+        }
         const bool cstart = jr == 0 || j == j0;
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
@@ -927,7 +952,8 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
 #endif
         int lds_bytes = R2CW2_LDS;
         if (walk == 3 && !dbg) { /* two walks per CU (k_r2c_walk1); the phase trace is walk2's */
-            fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>;
+            fw = env("HSFFT_R2C_PFH", 0) ? (sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>)
+                                         : (sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>);
             lds_bytes = R2CW1_LDS;
         }
         a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
