@@ -763,8 +763,9 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
 }
 
 /* PFH: the next tile's hi rows are loaded at the start of this tile's pairs phase, i.e. before
- * its store burst, so waiting for them does not wait for the stores (vmcnt is in order) */
-template <int SGN, bool PFH = false>
+ * its store burst, so waiting for them does not wait for the stores (vmcnt is in order); PFL:
+ * the lo rows are loaded at the start of the hi phase, while the hi tile is transformed */
+template <int SGN, bool PFH = false, bool PFL = false>
 __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -835,6 +836,8 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
         } else {
             w1_load(xr, xi, w, row, B, qhi, a.tw, tid);
         }
+        double lr[8], li[8]; /* PFL: the lo tile's rows */
+        if constexpr (PFL) w1_rows(lr, li, row, B, qlo, tid);
         __syncthreads(); /* the previous pairs phase has read the image */
         w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qhi, tid);
 #pragma unroll
@@ -843,7 +846,16 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
             him[jj] = xi[jj];
         }
         /* ---- lo(j) */
-        w1_load(xr, xi, w, row, B, qlo, a.tw, tid);
+        if constexpr (PFL) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                xr[i] = lr[i];
+                xi[i] = li[i];
+            }
+            tw_run(w, a.tw, B - 1 + 7 * (qlo + g));
+        } else {
+            w1_load(xr, xi, w, row, B, qlo, a.tw, tid);
+        }
         __syncthreads(); /* every wave's hi stage-2 twiddles are read back from the image */
         w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qlo, tid);
         __syncthreads();
@@ -952,8 +964,12 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
 #endif
         int lds_bytes = R2CW2_LDS;
         if (walk == 3 && !dbg) { /* two walks per CU (k_r2c_walk1); the phase trace is walk2's */
-            fw = env("HSFFT_R2C_PFH", 0) ? (sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>)
-                                         : (sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>);
+            switch (env("HSFFT_R2C_PFH", 0)) { /* bit 0: next hi rows before the stores, bit 1: lo rows with hi */
+            case 1: fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>; break;
+            case 2: fw = sgn == 1 ? k_r2c_walk1<1, false, true> : k_r2c_walk1<-1, false, true>; break;
+            case 3: fw = sgn == 1 ? k_r2c_walk1<1, true, true> : k_r2c_walk1<-1, true, true>; break;
+            default: fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>; break;
+            }
             lds_bytes = R2CW1_LDS;
         }
         a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */

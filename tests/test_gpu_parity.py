@@ -674,14 +674,16 @@ def test_r2c_walk(n, sgn, wt, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("order,wt,pfh", [("9", "8", "0"), ("0", "1", "0"), ("0", "5", "0"), ("0", "4096", "0"),
                                           ("2", "5", "0"), ("5", "16", "0"), ("1", "8", "0"), ("9", "32", "1"),
-                                          ("0", "1", "1"), ("2", "5", "1"), ("0", "4096", "1")])
+                                          ("0", "1", "1"), ("2", "5", "1"), ("0", "4096", "1"), ("9", "32", "3"),
+                                          ("0", "1", "3"), ("2", "5", "3"), ("0", "4096", "2")])
 @pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
 def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
     """pf::k_r2c_walk1 (HSFFT_R2C_WALK=3: the split walk sized for two workgroups per CU -- one
     tile buffer, stage-0/1 twiddles from global memory, 80 KiB of LDS): walk lengths 1 (every
     tile a walk's first), 5 (uneven walks), 4096 (one walk per row), the rotated and class
-    orders, segment-major order; pfh 1: the next hi tile's rows loaded before the pairs phase's
-    store burst; bit-exact vs the oracle, odd batch, stale output buffer."""
+    orders, segment-major order; pfh bit 0: the next hi tile's rows loaded before the pairs
+    phase's store burst, bit 1: the lo rows loaded with the hi phase; bit-exact vs the oracle, odd
+    batch, stale output buffer."""
     monkeypatch.setenv("HSFFT_R2C_WALK", "3")
     monkeypatch.setenv("HSFFT_R2C_WT", wt)
     monkeypatch.setenv("HSFFT_R2C_ORDER", order)
