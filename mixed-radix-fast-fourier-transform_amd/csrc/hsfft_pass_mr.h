@@ -997,10 +997,11 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * fused in registers as stages 0 and 1 are -- three exchanges per row instead of four */
         const char *e23 = getenv("HSFFT_ROW_F23");
         const bool f23 = e23 ? atoi(e23) != 0 : true;
-        /* F45 (HSFFT_ROW_F45): stages 4 and 5 ([7,8], 225 groups of 56 points) fused over thread
-         * pairs (DPP lane swaps): two exchanges per row */
+        /* F45 (HSFFT_ROW_F45, default 1 since round 4): stages 4 and 5 ([7,8], 225 groups of 56
+         * points) fused over thread pairs (DPP lane swaps): two exchanges per row; in-process A/B
+         * 5.97 vs 6.08 ms per 65536 rows (profiles/r04i_i_c3_f45.txt) */
         const char *e45 = getenv("HSFFT_ROW_F45");
-        const bool f45 = f23 && e45 && atoi(e45) != 0;
+        const bool f45 = f23 && (e45 ? atoi(e45) != 0 : true);
         kfn fn = f23 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true>
                                : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true>)
                      : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>

@@ -964,7 +964,10 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
 #endif
         int lds_bytes = R2CW2_LDS;
         if (walk == 3 && !dbg) { /* two walks per CU (k_r2c_walk1); the phase trace is walk2's */
-            switch (env("HSFFT_R2C_PFH", 0)) { /* bit 0: next hi rows before the stores, bit 1: lo rows with hi */
+            /* bit 0 (default on since round 4): the next hi tile's rows loaded before the pairs
+             * phase's stores, 20.00 vs 20.15 ms per 512 rows in-process; bit 1: the lo rows loaded
+             * with the hi phase, 20.11 (profiles/r04i_i_c5.txt) */
+            switch (env("HSFFT_R2C_PFH", 1)) {
             case 1: fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>; break;
             case 2: fw = sgn == 1 ? k_r2c_walk1<1, false, true> : k_r2c_walk1<-1, false, true>; break;
             case 3: fw = sgn == 1 ? k_r2c_walk1<1, true, true> : k_r2c_walk1<-1, true, true>; break;
@@ -1047,7 +1050,9 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
             *TL = env("HSFFT_PFQ", 4) > 0 ? env("HSFFT_PFQ", 4) : 4;
             *threads = 512;
             *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
-            if (env("HSFFT_PFA_NT", 0) & 2 && !l->conj) /* measurement: non-temporal output stores */
+            /* non-temporal output stores (HSFFT_PFA_NT bit 1, default on since round 4): 48.42 vs
+             * 49.48 ms per 4096 x 2^20 in-process (profiles/r04i_i_c2_nt.txt) */
+            if ((env("HSFFT_PFA_NT", 3) & 2) && !l->conj)
                 return l->sgn == 1 ? k_firstq<4, 3, 2, 1, false, true> : k_firstq<4, 3, 2, -1, false, true>;
             if (l->sgn == 1) return l->conj ? k_firstq<4, 3, 2, 1, true> : k_firstq<4, 3, 2, 1, false>;
             return l->conj ? k_firstq<4, 3, 2, -1, true> : k_firstq<4, 3, 2, -1, false>;
@@ -1067,7 +1072,7 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
              * XCD's 64 workgroups write per column group no longer evict the input lines their
              * neighbours still have to read -- FETCH -17 %, pass A 7.29 -> 7.01 ms per 512 rows,
              * c5 21.44 -> 21.12 ms (profiles/r04g_*) */
-            if ((env("HSFFT_PFA_NT", 1) & 1) && !l->conj)
+            if ((env("HSFFT_PFA_NT", 3) & 1) && !l->conj)
                 return l->sgn == 1 ? k_firstq<8, 3, 1, 1, false, true> : k_firstq<8, 3, 1, -1, false, true>;
             if (l->sgn == 1) return l->conj ? k_firstq<8, 3, 1, 1, true> : k_firstq<8, 3, 1, 1, false>;
             return l->conj ? k_firstq<8, 3, 1, -1, true> : k_firstq<8, 3, 1, -1, false>;

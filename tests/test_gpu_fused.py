@@ -68,8 +68,8 @@ def test_pipelined_passes_bit_exact(pf, monkeypatch):
 
 @pytest.mark.parametrize("nt", ["0", "2"])
 def test_first_pass_2p20_nt_stores(nt, monkeypatch):
-    """2^20's pass A (k_firstq<4,3,2>) with non-temporal output stores (HSFFT_PFA_NT bit 1):
-    bit-exact, both signs"""
+    """2^20's pass A (k_firstq<4,3,2>) with plain / non-temporal (default) output stores
+    (HSFFT_PFA_NT bit 1): bit-exact, both signs"""
     monkeypatch.setenv("HSFFT_PFA_NT", nt)
     x = T.complex_input(N, 0xF00D, batch=3).reshape(3, N)
     for sgn in (1, -1):

@@ -699,7 +699,7 @@ def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "1"}])
+@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
