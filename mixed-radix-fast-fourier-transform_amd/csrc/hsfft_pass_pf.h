@@ -268,7 +268,7 @@ __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], cons
     }
 }
 
-template <int T, int SGN, bool CONJ>
+template <int T, int SGN, bool CONJ, bool NTS = false>
 __global__ __launch_bounds__(512, 4) void k_b512(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
             xr[i] = v.x;
             xi[i] = v.y;
         }
-        b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
+        b512_body<SGN, NTS>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
     }
 }
 
@@ -1089,7 +1089,9 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
         switch (*TL) {
         case 32: return b512_fn<32>(l->sgn, l->conj);
         case 16: return b512_fn<16>(l->sgn, l->conj);
-        case 8: return b512_fn<8>(l->sgn, l->conj);
+        case 8: /* HSFFT_PFB_NT=1 (measurement): non-temporal output stores */
+            if (env("HSFFT_PFB_NT", 0) == 1 && !l->conj) return l->sgn == 1 ? k_b512<8, 1, false, true> : k_b512<8, -1, false, true>;
+            return b512_fn<8>(l->sgn, l->conj);
         case 4: return b512_fn<4>(l->sgn, l->conj);
         default: return b512_fn<2>(l->sgn, l->conj);
         }

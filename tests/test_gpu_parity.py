@@ -699,7 +699,8 @@ def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"}])
+@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
+                                 {"HSFFT_ROW_NT": "1"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -707,9 +708,10 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     row-walking grid uneven (300 rows over 256 workgroups); 64 rows give every workgroup
     exactly ONE row, so no row can lean on an earlier row's barriers (the stage-1 twiddles of
     the fused first stages are read right after the per-workgroup LDS copy).  Schedules:
-    mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, the next row's
-    first input group prefetched into registers), the same without the stage 2-3 fusion, and
-    the two mixed-radix passes, and stages 4-5 fused over thread pairs (F45)."""
+    mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, stages 4-5 fused
+    over thread pairs (F45), the next row's first input group prefetched into registers), the
+    same with stages 4 and 5 apart, without the stage 2-3 fusion, with non-temporal row
+    stores, and the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600
