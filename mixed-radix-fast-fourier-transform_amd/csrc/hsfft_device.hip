@@ -866,6 +866,8 @@ int hsd_select_stream(int idx)
     return 0;
 }
 
+int hsd_stream_index(void) { return t_sidx; }
+
 int hsd_h2d_async(void *d, const void *h, size_t bytes)
 {
     HCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream()));

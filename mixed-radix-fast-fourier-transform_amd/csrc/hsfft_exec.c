@@ -898,6 +898,36 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
         return 1; /* HSFFT_R2C_FUSE=0: pass B + k_r2c_post2 (r2c 2^22: 85 vs 93 GSamples/s fused) */
     hs_devstate *ds = devstate(e);
     if (!ds) return HSFFT_ERR_DEVICE;
+    /* HSFFT_R2C_OVL = S (measurement): the call in sub-chunks of S rows, pass A of every
+     * sub-chunk on the library stream and the split walk of sub-chunk s on the pipeline stream
+     * behind pass A(s) only, so the walks (latency-bound) overlap the later pass As
+     * (bandwidth-bound); Z holds every row, so nothing is reused; the library stream then waits
+     * for the last walk */
+    const int ovl = env_int("HSFFT_R2C_OVL", 0);
+    if (ovl > 0 && batch > ovl && hsd_stream_index() == 0) {
+        const int ns = (batch + ovl - 1) / ovl;
+        int rc = 0;
+        for (int s = 0; s < ns && !rc; s++) {
+            const long long r0 = (long long)s * ovl;
+            const int nb = (int)(batch - r0 < ovl ? batch - r0 : ovl);
+            void *Zs = (char *)Z + r0 * e->M * (long long)sizeof(fft_data);
+            hsd_select_stream(0);
+            rc = launch_pass(e, ds, 0, (const char *)in + r0 * idist * (long long)sizeof(fft_data), idist, Zs, e->M,
+                             nb, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN, NULL, e->M);
+            if (!rc) rc = hsd_event_record(2 * s) ? HSFFT_ERR_DEVICE : 0;
+            hsd_select_stream(1);
+            if (!rc) rc = hsd_event_wait(2 * s) ? HSFFT_ERR_DEVICE : 0;
+            if (!rc && hsd_r2c_last(Zs, e->M, (char *)X + r0 * xdist * (long long)sizeof(fft_data), xdist, ds->d_tw,
+                                    tw2, e->M, p1->B, nb, e->sgn, compact)) {
+                hs_seterr("r2c last pass: %s", hsd_errstr());
+                rc = HSFFT_ERR_DEVICE;
+            }
+            if (!rc) rc = hsd_event_record(2 * s + 1) ? HSFFT_ERR_DEVICE : 0;
+        }
+        hsd_select_stream(0);
+        if (!rc) rc = hsd_event_wait(2 * (ns - 1) + 1) ? HSFFT_ERR_DEVICE : 0;
+        return rc;
+    }
     int rc = launch_pass(e, ds, 0, in, idist, Z, e->M, batch, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN,
                          NULL, e->M);
     if (!rc && hsd_r2c_last(Z, e->M, X, xdist, ds->d_tw, tw2, e->M, p1->B, batch, e->sgn, compact)) {

@@ -84,6 +84,7 @@ int hsd_memset_async(void *d, int v, size_t bytes);
 int hsd_sync(void);
 int hsd_sync_spin(void);          /* the same, polling instead of a blocking wait */
 int hsd_select_stream(int idx);   /* 0 library stream, 1 pipeline / H2D, 2 D2H, 3 this thread's own stream */
+int hsd_stream_index(void);       /* the calling thread's selected stream */
 int hsd_h2d_async(void *d, const void *h, size_t bytes);   /* on the selected stream */
 int hsd_d2h_async(void *h, const void *d, size_t bytes);
 int hsd_stream_sync(void);        /* the selected stream */

@@ -699,6 +699,46 @@ def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,batch,ovl", [(1 << 22, 5, 2), (1 << 17, 7, 3), (1 << 17, 4, 1)])
+def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
+    """HSFFT_R2C_OVL: pass A of each sub-chunk on the library stream, the split walk on the
+    pipeline stream behind it (uneven last sub-chunk, one-row sub-chunks); bit-exact vs the
+    oracle, and the library stream is ordered after the last walk (a second call into the
+    same buffers right after must see the first call's rows complete)"""
+    monkeypatch.setenv("HSFFT_R2C_OVL", str(ovl))
+    x = T.real_input(n, 35, batch=batch).reshape(batch, n)
+    rp = hsfft.RealPlan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(batch * n * 16)
+    hsfft.fill_complex(dout, batch * n, 1)
+    hsfft.r2c_batched(rp, din, dout, batch)
+    y1 = dout.to_array(np.complex128).reshape(batch, n)
+    hsfft.r2c_batched(rp, din, dout, batch)
+    y2 = dout.to_array(np.complex128).reshape(batch, n)
+    ref = T.oracle_r2c(x, 1)
+    assert T.bits_equal(y1, ref)
+    assert T.bits_equal(y2, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wt", ["32", "5"])
+@pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 17, -1)])
+def test_r2c_walk1_nt_stores(n, sgn, wt, monkeypatch):
+    """k_r2c_walk1 (default prefetch) with non-temporal pairs-phase stores (HSFFT_R2C_NTW=1):
+    bit-exact vs the oracle, odd batch, stale output buffer"""
+    monkeypatch.setenv("HSFFT_R2C_NTW", "1")
+    monkeypatch.setenv("HSFFT_R2C_WT", wt)
+    x = T.real_input(n, 33, batch=3).reshape(3, n)
+    rp = hsfft.RealPlan(n, sgn)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(3 * n * 16)
+    hsfft.fill_complex(dout, 3 * n, 1)
+    hsfft.r2c_batched(rp, din, dout, 3)
+    y = dout.to_array(np.complex128).reshape(3, n)
+    assert T.bits_equal(y, T.oracle_r2c(x, sgn))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
                                  {"HSFFT_ROW_NT": "1"}])
 @pytest.mark.parametrize("sgn", [1, -1])
