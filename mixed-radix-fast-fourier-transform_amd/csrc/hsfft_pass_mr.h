@@ -604,7 +604,7 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 }
 
 /* stages 4 (radix 7) and 5 (radix 8) of the pair's group, then the row's stores */
-template <int P, int TPG, bool CONJ, bool NTS = false>
+template <int P, int TPG, bool CONJ>
 __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const double2 *ltw, const double2 *tw,
                                              double2 *out, int jt, int sgn)
 {
@@ -653,10 +653,7 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
         hsb::bfly<8>(zr, zi, sgn, false);
         if (live && (h == 0 || d < 3)) {
 #pragma unroll
-            for (int j5 = 0; j5 < 8; j5++) {
-                if constexpr (NTS) pf::stg_nt(out, (k + (unsigned)j5 * L5) * 16u, make_double2(zr[j5], zi[j5]));
-                else pf::stg(out, (k + (unsigned)j5 * L5) * 16u, make_double2(zr[j5], zi[j5]));
-            }
+            for (int j5 = 0; j5 < 8; j5++) pf::stg(out, (k + (unsigned)j5 * L5) * 16u, make_double2(zr[j5], zi[j5]));
         }
     }
 }
@@ -746,7 +743,7 @@ constexpr int ROW_PRE_PTS = 8448;
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false, bool F45 = false, bool NTS = false>
+          bool F23 = false, bool F45 = false>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
@@ -844,7 +841,7 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
             mark(a, tp, 3);
-            fused45_pair<P, TPG, CONJ, NTS>(xr, xi, ltw, a.tw, out, jt, sgn);
+            fused45_pair<P, TPG, CONJ>(xr, xi, ltw, a.tw, out, jt, sgn);
             mark(a, tp, 6);
             if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + 7] += 1;
             continue;
@@ -1012,8 +1009,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         if (f45)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true>;
-        const char *ent = getenv("HSFFT_ROW_NT"); /* measurement: non-temporal row stores (F45) */
-        if (f45 && !a.conj && ent && atoi(ent) == 1) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, true>;
+        /* non-temporal row stores measured slower: 6.32 vs 5.96 ms (round 4, removed) */
         const int threads = 512;
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));

@@ -268,7 +268,7 @@ __device__ __forceinline__ void b512_body(double (&xr)[8], double (&xi)[8], cons
     }
 }
 
-template <int T, int SGN, bool CONJ, bool NTS = false>
+template <int T, int SGN, bool CONJ>
 __global__ __launch_bounds__(512, 4) void k_b512(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(512, 4) void k_b512(Args a)
             xr[i] = v.x;
             xi[i] = v.y;
         }
-        b512_body<SGN, NTS>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
+        b512_body<SGN>(xr, xi, w2, lds, ltw, a.out + (long long)b * a.odist, B, lane, jt, g);
     }
 }
 
@@ -686,14 +686,6 @@ __global__ __launch_bounds__(512, 2) void k_r2c_walk2(Args a, unsigned h, unsign
  * (every load issued after a store burst waits for that burst: vmcnt is in order). */
 constexpr int R2CW1_LDS = (512 * 8 + 1024) * 16;
 
-/* one output entry, plain or non-temporal (NTS) */
-template <bool NTS>
-__device__ __forceinline__ void st2(double2 *X, unsigned i, double2 v)
-{
-    if constexpr (NTS) stg_nt(X + i, 0u, v);
-    else X[i] = v;
-}
-
 /* a run of 7 twiddles at table index idx (stage 0: B - 1 + 7q; stage 1: 8B - 1 + 7(q + B kl)) */
 __device__ __forceinline__ void tw_run(double2 (&w)[7], const double2 *tw, unsigned idx)
 {
@@ -773,7 +765,7 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
 /* PFH: the next tile's hi rows are loaded at the start of this tile's pairs phase, i.e. before
  * its store burst, so waiting for them does not wait for the stores (vmcnt is in order); PFL:
  * the lo rows are loaded at the start of the hi phase, while the hi tile is transformed */
-template <int SGN, bool PFH = false, bool PFL = false, bool NTS = false>
+template <int SGN, bool PFH = false, bool PFL = false>
 __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -884,17 +876,17 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
             double re, im, re2, im2;
             r8::r2c_pair(zk, zh, w2t[k], re, im);
             r8::r2c_pair(zh, zk, w2t[hk], re2, im2);
-            st2<NTS>(X, N - k, make_double2(re, -im));
-            st2<NTS>(X, hk, make_double2(re2, im2));
+            X[N - k] = make_double2(re, -im);
+            X[hk] = make_double2(re2, im2);
             const double2 va = grp_shift<-1>(make_double2(re, im)), vb = grp_shift<-1>(make_double2(re2, -im2));
             const unsigned p = u * B + 8 * j + g;
             if (g != 0) {
-                st2<NTS>(X, p, va);
-                st2<NTS>(X, h + p, vb);
+                X[p] = va;
+                X[h + p] = vb;
             } else {
                 if (!cstart) {
-                    st2<NTS>(X, p, cry[u]);
-                    st2<NTS>(X, h + p, cry[512 + u]);
+                    X[p] = cry[u];
+                    X[h + p] = cry[512 + u];
                 } else if (jr != 0 && j1 < B / 16) { /* the first chain's carry: bin 8*j1 */
                     X[u * B + 8 * j1] = cry[u];
                     X[h + u * B + 8 * j1] = cry[512 + u];
@@ -976,11 +968,7 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
              * phase's stores, 20.00 vs 20.15 ms per 512 rows in-process; bit 1: the lo rows loaded
              * with the hi phase, 20.11 (profiles/r04i_i_c5.txt) */
             switch (env("HSFFT_R2C_PFH", 1)) {
-            case 1:
-                /* HSFFT_R2C_NTW=1 (measurement): non-temporal pairs-phase stores */
-                if (env("HSFFT_R2C_NTW", 0) == 1) fw = sgn == 1 ? k_r2c_walk1<1, true, false, true> : k_r2c_walk1<-1, true, false, true>;
-                else fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>;
-                break;
+            case 1: fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>; break;
             case 2: fw = sgn == 1 ? k_r2c_walk1<1, false, true> : k_r2c_walk1<-1, false, true>; break;
             case 3: fw = sgn == 1 ? k_r2c_walk1<1, true, true> : k_r2c_walk1<-1, true, true>; break;
             default: fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>; break;
@@ -1101,9 +1089,7 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
         switch (*TL) {
         case 32: return b512_fn<32>(l->sgn, l->conj);
         case 16: return b512_fn<16>(l->sgn, l->conj);
-        case 8: /* HSFFT_PFB_NT=1 (measurement): non-temporal output stores */
-            if (env("HSFFT_PFB_NT", 0) == 1 && !l->conj) return l->sgn == 1 ? k_b512<8, 1, false, true> : k_b512<8, -1, false, true>;
-            return b512_fn<8>(l->sgn, l->conj);
+        case 8: return b512_fn<8>(l->sgn, l->conj);
         case 4: return b512_fn<4>(l->sgn, l->conj);
         default: return b512_fn<2>(l->sgn, l->conj);
         }

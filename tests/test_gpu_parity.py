@@ -721,26 +721,7 @@ def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wt", ["32", "5"])
-@pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 17, -1)])
-def test_r2c_walk1_nt_stores(n, sgn, wt, monkeypatch):
-    """k_r2c_walk1 (default prefetch) with non-temporal pairs-phase stores (HSFFT_R2C_NTW=1):
-    bit-exact vs the oracle, odd batch, stale output buffer"""
-    monkeypatch.setenv("HSFFT_R2C_NTW", "1")
-    monkeypatch.setenv("HSFFT_R2C_WT", wt)
-    x = T.real_input(n, 33, batch=3).reshape(3, n)
-    rp = hsfft.RealPlan(n, sgn)
-    din = hsfft.DeviceBuffer.from_array(x)
-    dout = hsfft.DeviceBuffer(3 * n * 16)
-    hsfft.fill_complex(dout, 3 * n, 1)
-    hsfft.r2c_batched(rp, din, dout, 3)
-    y = dout.to_array(np.complex128).reshape(3, n)
-    assert T.bits_equal(y, T.oracle_r2c(x, sgn))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
-                                 {"HSFFT_ROW_NT": "1"}])
+@pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -750,8 +731,8 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     the fused first stages are read right after the per-workgroup LDS copy).  Schedules:
     mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, stages 4-5 fused
     over thread pairs (F45), the next row's first input group prefetched into registers), the
-    same with stages 4 and 5 apart, without the stage 2-3 fusion, with non-temporal row
-    stores, and the two mixed-radix passes."""
+    same with stages 4 and 5 apart, without the stage 2-3 fusion, and the two mixed-radix
+    passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600

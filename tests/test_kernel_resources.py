@@ -25,22 +25,22 @@ BUDGETS = [
     # 2^20 pass A (c2): 512 threads, 2 workgroups per CU need 4 waves per SIMD
     (r"^_ZN2pf8k_firstqILi4ELi3ELi2ELin?1ELb[01]ELb0EE", 0, 128, 4),
     # 2^20 pass B (c2)
-    (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]ELb[01]EE", 0, 112, 4),
+    (r"^_ZN2pf6k_b512ILi8ELin?1ELb[01]EE", 0, 112, 4),
     # 2^21 pass A (c5)
     (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]ELb[01]EE", 0, 128, 4),
     # r2c split walk (c5, default since round 4: the next hi tile's rows loaded before the
     # stores, HSFFT_R2C_PFH=1): two 512-thread workgroups per CU, 128 VGPRs, no spill
-    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELb[01]EE", 0, 128, 4),
+    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0EE", 0, 128, 4),
     # its other prefetch variants: at most one dword of spill (PFH=0: reloaded where the
     # stage-2 twiddles are waited for anyway)
-    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb[01]ELb[01]ELb[01]EE", 1, 128, 4),
+    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb[01]ELb[01]EE", 1, 128, 4),
     # the one-per-CU walk (HSFFT_R2C_WALK=2): up to 256 VGPRs
     (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0, 256, 2),
     # 12600 row kernel (c3, default since round 4: stages 4-5 fused over thread pairs,
     # HSFFT_ROW_F45=1): one 512-thread workgroup per CU
-    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb1ELb[01]EE", 0, 256, 2),
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb1EE", 0, 256, 2),
     # the same with stages 4 and 5 apart (HSFFT_ROW_F45=0)
-    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb0ELb0EE", 0, 256, 2),
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb0EE", 0, 256, 2),
     # persistent Bluestein (c4): the whole grid (2 workgroups per CU) must be resident, so
     # 128 VGPRs is a hard limit; 8 dwords of spill are intrinsic (also compiled alone)
     (r"^_ZN3bxc6k_bxcdILin?1EE", 8, 128, 4),
