@@ -707,6 +707,34 @@ __device__ __forceinline__ void redistribute_at(double2 (&w)[7], double2 *region
     for (int i = 0; i < 7; i++) w[i] = reg[(lane & 7) * 7 + i];
 }
 
+/* PROBE (timing probes of k_r2c_walk1, -DHSFFT_DEV_PROBES builds only; results wrong): bit 0 no
+ * twiddle2 loads, bit 1 no stage twiddle loads, bit 2 no stage arithmetic (the twiddles are
+ * folded in with one add each so that their loads stay), bit 3 no exchanges / redistribution,
+ * bit 4 no output stores (kept behind a condition that is false at run time) */
+template <int PROBE>
+__device__ __forceinline__ void p_tw_run(double2 (&w)[7], const double2 *tw, unsigned idx)
+{
+    if constexpr (PROBE & 2) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) w[i] = make_double2(0.5 + i, 0.25 - i);
+    } else {
+        tw_run(w, tw, idx);
+    }
+}
+template <int PROBE, int SGN>
+__device__ __forceinline__ void p_stage(double (&xr)[8], double (&xi)[8], const double2 (&w)[7])
+{
+    if constexpr (PROBE & 4) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            xr[i + 1] += w[i].x;
+            xi[i + 1] += w[i].y;
+        }
+    } else {
+        stage<8, SGN>(xr, xi, w, false);
+    }
+}
+
 /* one tile's row loads */
 __device__ __forceinline__ void w1_rows(double (&xr)[8], double (&xi)[8], const double2 *row, unsigned B, unsigned q0,
                                         unsigned tid)
@@ -723,11 +751,12 @@ __device__ __forceinline__ void w1_rows(double (&xr)[8], double (&xi)[8], const 
 }
 
 /* one tile's row loads and its stage-0 run (registers) */
+template <int PROBE = 0>
 __device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double2 (&w)[7], const double2 *row,
                                         unsigned B, unsigned q0, const double2 *tw, unsigned tid)
 {
     w1_rows(xr, xi, row, B, q0, tid);
-    tw_run(w, tw, B - 1 + 7 * (q0 + (tid & 7)));
+    p_tw_run<PROBE>(w, tw, B - 1 + 7 * (q0 + (tid & 7)));
 }
 
 /* the tile's three stages with one twiddle run live at a time (<= 128 VGPRs with the hi tile's
@@ -735,7 +764,7 @@ __device__ __forceinline__ void w1_load(double (&xr)[8], double (&xi)[8], double
  * the coalesced stage-2 run after the second and redistributed through the
  * image's first half (waves 0-3, then 4-7: the second half may hold the hi tile's real parts);
  * split exchanges through doubles [0, 4096) */
-template <int SGN>
+template <int SGN, int PROBE = 0>
 __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], double2 (&w)[7], double2 *lds,
                                           const double2 *tw, unsigned B, unsigned q0, unsigned tid0)
 {
@@ -743,29 +772,33 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
     unsigned tid = tid0;
     asm volatile("" : "+v"(tid));
     const unsigned g = tid & 7, jt = tid >> 3;
-    stage<8, SGN>(xr, xi, w, false);
-    r8::exchange<8, 1, 8, TPG, P, G, true>(xr, xi, lds, jt, g);
-    tw_run(w, tw, 8 * B - 1 + 7 * (q0 + g + B * (jt & 7))); /* after the exchange: issued earlier,
-                                                                * its 28 VGPRs spill (19 dwords) */
-    stage<8, SGN>(xr, xi, w, false);
-    r8::exchange<8, 8, 8, TPG, P, G, true>(xr, xi, lds, jt, g); /* ends with a barrier: the image is free */
-    {
+    p_stage<PROBE, SGN>(xr, xi, w);
+    if constexpr (!(PROBE & 8)) r8::exchange<8, 1, 8, TPG, P, G, true>(xr, xi, lds, jt, g);
+    p_tw_run<PROBE>(w, tw, 8 * B - 1 + 7 * (q0 + g + B * (jt & 7))); /* after the exchange: issued
+                                                                        * earlier, its 28 VGPRs spill */
+    p_stage<PROBE, SGN>(xr, xi, w);
+    if constexpr (!(PROBE & 8)) r8::exchange<8, 8, 8, TPG, P, G, true>(xr, xi, lds, jt, g); /* ends with a barrier */
+    if constexpr (!(PROBE & 2)) {
         r8::Args ta;
         ta.tw = tw;
         ta.B = B;
         r8::load_tw_co<64>(w, ta, (int)jt, q0);
+    } else {
+        p_tw_run<PROBE>(w, tw, 0);
     }
-    const unsigned wave = tid0 >> 6;
-    if (wave < 4) redistribute_at(w, lds + wave * 448);
-    __syncthreads();
-    if (wave >= 4) redistribute_at(w, lds + (wave - 4) * 448);
-    stage<8, SGN>(xr, xi, w, false);
+    if constexpr (!(PROBE & 8)) {
+        const unsigned wave = tid0 >> 6;
+        if (wave < 4) redistribute_at(w, lds + wave * 448);
+        __syncthreads();
+        if (wave >= 4) redistribute_at(w, lds + (wave - 4) * 448);
+    }
+    p_stage<PROBE, SGN>(xr, xi, w);
 }
 
 /* PFH: the next tile's hi rows are loaded at the start of this tile's pairs phase, i.e. before
  * its store burst, so waiting for them does not wait for the stores (vmcnt is in order); PFL:
  * the lo rows are loaded at the start of the hi phase, while the hi tile is transformed */
-template <int SGN, bool PFH = false, bool PFL = false>
+template <int SGN, bool PFH = false, bool PFL = false, int PROBE = 0>
 __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -832,14 +865,14 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
                 xr[i] = pr[i];
                 xi[i] = pi[i];
             }
-            tw_run(w, a.tw, B - 1 + 7 * (qhi + g));
+            p_tw_run<PROBE>(w, a.tw, B - 1 + 7 * (qhi + g));
         } else {
-            w1_load(xr, xi, w, row, B, qhi, a.tw, tid);
+            w1_load<PROBE>(xr, xi, w, row, B, qhi, a.tw, tid);
         }
         double lr[8], li[8]; /* PFL: the lo tile's rows */
         if constexpr (PFL) w1_rows(lr, li, row, B, qlo, tid);
         __syncthreads(); /* the previous pairs phase has read the image */
-        w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qhi, tid);
+        w1_stages<SGN, PROBE>(xr, xi, w, lds, a.tw, B, qhi, tid);
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) {
             ld[4096 + (jt + jj * TPG) * G + g] = xr[jj]; /* hi real parts wait in the image's second half */
@@ -852,12 +885,12 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
                 xr[i] = lr[i];
                 xi[i] = li[i];
             }
-            tw_run(w, a.tw, B - 1 + 7 * (qlo + g));
+            p_tw_run<PROBE>(w, a.tw, B - 1 + 7 * (qlo + g));
         } else {
-            w1_load(xr, xi, w, row, B, qlo, a.tw, tid);
+            w1_load<PROBE>(xr, xi, w, row, B, qlo, a.tw, tid);
         }
         __syncthreads(); /* every wave's hi stage-2 twiddles are read back from the image */
-        w1_stages<SGN>(xr, xi, w, lds, a.tw, B, qlo, tid);
+        w1_stages<SGN, PROBE>(xr, xi, w, lds, a.tw, B, qlo, tid);
         __syncthreads();
 #pragma unroll
         for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
@@ -874,17 +907,24 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
             const unsigned sl = (P - 1 - u) * G + (7 - g);
             const double2 zk = make_double2(xr[jj], xi[jj]), zh = make_double2(ld[4096 + sl], ld[sl]);
             double re, im, re2, im2;
-            r8::r2c_pair(zk, zh, w2t[k], re, im);
-            r8::r2c_pair(zh, zk, w2t[hk], re2, im2);
-            X[N - k] = make_double2(re, -im);
-            X[hk] = make_double2(re2, im2);
+            const double2 wk = (PROBE & 1) ? make_double2(0.5, 0.25) : w2t[k];
+            const double2 whk = (PROBE & 1) ? make_double2(0.25, 0.5) : w2t[hk];
+            r8::r2c_pair(zk, zh, wk, re, im);
+            r8::r2c_pair(zh, zk, whk, re2, im2);
+            const bool st = !(PROBE & 16) || h == 0; /* h > 0 always: the probe stores nothing */
+            if (st) {
+                X[N - k] = make_double2(re, -im);
+                X[hk] = make_double2(re2, im2);
+            }
             const double2 va = grp_shift<-1>(make_double2(re, im)), vb = grp_shift<-1>(make_double2(re2, -im2));
             const unsigned p = u * B + 8 * j + g;
             if (g != 0) {
-                X[p] = va;
-                X[h + p] = vb;
+                if (st) {
+                    X[p] = va;
+                    X[h + p] = vb;
+                }
             } else {
-                if (!cstart) {
+                if (!cstart && st) {
                     X[p] = cry[u];
                     X[h + p] = cry[512 + u];
                 } else if (jr != 0 && j1 < B / 16) { /* the first chain's carry: bin 8*j1 */
@@ -974,6 +1014,19 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
             default: fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>; break;
             }
             lds_bytes = R2CW1_LDS;
+#ifdef HSFFT_DEV_PROBES
+            /* HSFFT_R2C_W1PROBE (timing only, results wrong; the default PFH walk, sgn 1): see PROBE */
+            switch (sgn == 1 ? env("HSFFT_R2C_W1PROBE", 0) : 0) {
+            case 3: fw = k_r2c_walk1<1, true, false, 3>; break;
+            case 4: fw = k_r2c_walk1<1, true, false, 4>; break;
+            case 8: fw = k_r2c_walk1<1, true, false, 8>; break;
+            case 12: fw = k_r2c_walk1<1, true, false, 12>; break;
+            case 15: fw = k_r2c_walk1<1, true, false, 15>; break;
+            case 16: fw = k_r2c_walk1<1, true, false, 16>; break;
+            case 31: fw = k_r2c_walk1<1, true, false, 31>; break;
+            default: break;
+            }
+#endif
         }
         a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
         static unsigned *s_dbg = nullptr;
