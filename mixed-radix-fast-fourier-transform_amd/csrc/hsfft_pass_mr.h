@@ -356,20 +356,11 @@ __device__ __forceinline__ void f01_load0(double2 (&p0)[PFG * R0 * R1], const do
     }
 }
 
-/* DMA layout (k_row2 DMA): groups ml >= HAS0*TPG of a row prefetched into LDS as R0*R1 runs
- * (run r = j1 + R1*i holds points ml + S*r, since NBF0 = R1*S), each padded to whole waves */
-template <int R0, int R1, int P, int TPG, int HAS0>
-struct DmaRuns {
-    static constexpr int S = P / (R0 * R1), ML0 = HAS0 * TPG, LEN = S - ML0, PITCH = (LEN + 63) / 64 * 64,
-                         NRUN = R0 * R1, CHUNKS = PITCH / 64;
-};
-
 template <int R0, int R1, int P, int TPG, bool CONJ, int HAS0 = 0>
 __device__ __forceinline__ void fused01(double *xr, double *xi, const double2 *in, const double2 *ltw, double *ld,
-                                        int jt, int sgn, const double2 *p0 = nullptr, const double2 *pre = nullptr)
+                                        int jt, int sgn, const double2 *p0 = nullptr)
 {
     constexpr int S = P / (R0 * R1), NG = cdiv(S, TPG), NBF0 = P / R0, Q = R0 * R1;
-    using DR = DmaRuns<R0, R1, P, TPG, HAS0>;
 #pragma unroll
     for (int g = 0; g < NG; g++) {
         int ml = g * TPG + jt;
@@ -380,9 +371,7 @@ __device__ __forceinline__ void fused01(double *xr, double *xi, const double2 *i
         for (int j1 = 0; j1 < R1; j1++)
 #pragma unroll
             for (int i = 0; i < R0; i++) {
-                const double2 v = g < HAS0 ? p0[(g * R1 + j1) * R0 + i]
-                                  : pre    ? pre[(j1 + R1 * i) * DR::PITCH + ml - DR::ML0]
-                                           : pf::ldg(in, (unsigned)(ml + S * j1 + i * NBF0) * 16u);
+                const double2 v = g < HAS0 ? p0[(g * R1 + j1) * R0 + i] : pf::ldg(in, (unsigned)(ml + S * j1 + i * NBF0) * 16u);
                 yr[j1 * R0 + i] = v.x;
                 yi[j1 * R0 + i] = v.y;
             }
@@ -753,16 +742,11 @@ constexpr int ROW_PRE_PTS = 8448;
 /* PF: the inputs of the next row's first PF 9-point groups (37 % of a row per group at
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
-/* DMA (with F45 and PF = 1): the next row's remaining fused01 groups (ml >= TPG, 63 % of a row)
- * are copied into LDS by LDS-DMA right after this row's last exchange, i.e. before this row's
- * stores, so that they do not queue behind the store burst (vmcnt is in order); the next row
- * reads them from LDS after one vmcnt(0) + barrier.  LDS: [ltw | image / prefetch runs]. */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false, bool F45 = false, bool DMA = false>
+          bool F23 = false, bool F45 = false>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
-    static_assert(!DMA || (F45 && PF == 1 && !PRE), "DMA: the F45 kernel with the one-group register prefetch");
     static_assert(PF == 0 || (F01 && !PRE), "PF prefetches fused01's first groups");
     static_assert(!F23 || (F01 && !PRE), "F23 follows fused01");
     using LS = List6<R0, R1, R2, R3, R4, R5>;
@@ -775,13 +759,8 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     static_assert(!PRE || (F01 && NT % 2 == 0 && 2 * NT * 8 + ROW_PRE_PTS * 16 <= 160 * 1024 &&
                            ROW_PRE_PTS >= 2 * (P / R0) && P * 8 <= ROW_PRE_PTS * 16),
                   "row prefetch layout");
-    using DR = DmaRuns<R0, R1, P, TPG, PF>;
-    static_assert(!DMA || (NT % 2 == 0 && 2 * NT * 8 + DR::NRUN * DR::PITCH * 16 <= 160 * 1024 &&
-                           P * 8 <= DR::NRUN * DR::PITCH * 16),
-                  "DMA layout");
-    double2 *ltw = (PRE || DMA) ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + P + (P & 1));
-    double *img = (PRE || DMA) ? ldsd + 2 * NT : ldsd;
-    bool dpre = false; /* DMA: this row's groups ml >= TPG are in the image area */
+    double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + P + (P & 1));
+    double *img = PRE ? ldsd + 2 * NT : ldsd;
     const int jt0 = threadIdx.x, sgn = a.sgn;
     /* LDS copy of the stage-1..4 twiddles, transposed within each stage's block [L-1, RL-1):
      * entry (k, i) at L-1 + (i-1)*L + k, so the lanes of a wave (consecutive k) read
@@ -816,17 +795,10 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         double2 *out = a.out + (long long)b * a.odist;
         double xr[NM], xi[NM];
         if constexpr (F01) {
-            if (PRE && pre) {
+            if (PRE && pre)
                 fused01p<R0, R1, P, TPG, CONJ>(xr, xi, in, ltw, reinterpret_cast<const double2 *>(img), jt, sgn);
-            } else if (DMA && dpre) {
-                /* every wave's LDS-DMA has landed (vmcnt(0) per wave, then the barrier: hipcc
-                 * puts its own vmcnt(0) after s_barrier) */
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                fused01<R0, R1, P, TPG, CONJ, PF>(xr, xi, in, ltw, img, jt, sgn, p0, reinterpret_cast<const double2 *>(img));
-            } else {
+            else
                 fused01<R0, R1, P, TPG, CONJ, PF>(xr, xi, in, ltw, img, jt, sgn, p0);
-            }
             if (a.dbg) {
                 r8::pin(*reinterpret_cast<double(*)[8]>(xr));
                 mark(a, tp, 0); /* loads + stages 0-1 */
@@ -869,22 +841,6 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
             mark(a, tp, 3);
-            if constexpr (DMA) {
-                const unsigned bn = b + gridDim.x;
-                dpre = bn < (unsigned)a.batch;
-                if (dpre) {
-                    __syncthreads(); /* every wave has read the image */
-                    const double2 *inn = a.in + (long long)bn * a.idist;
-                    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-                    double2 *dst = reinterpret_cast<double2 *>(img);
-#pragma unroll 1
-                    for (unsigned j = wave; j < (unsigned)(DR::NRUN * DR::CHUNKS); j += TPG / 64) {
-                        const unsigned r = j / DR::CHUNKS, c = j % DR::CHUNKS, e = c * 64 + lane;
-                        const unsigned src = r * DR::S + DR::ML0 + (e < (unsigned)DR::LEN ? e : DR::LEN - 1);
-                        glds16(inn + src, dst + r * DR::PITCH + c * 64);
-                    }
-                }
-            }
             fused45_pair<P, TPG, CONJ>(xr, xi, ltw, a.tw, out, jt, sgn);
             mark(a, tp, 6);
             if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + 7] += 1;
@@ -1027,7 +983,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     }
     if (v->row) { /* 12600 = [3,3,5,5,7,8]: k_row2 (the only whole-row variant) */
         constexpr int P = 12600, NT = 1574;
-        const size_t lds0 = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
+        const size_t lds = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
         if (l->batch <= 0) {
             snprintf(g_err, sizeof g_err, "mr: bad row batch=%d", l->batch);
             return -1;
@@ -1053,17 +1009,9 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         if (f45)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true>;
-        /* HSFFT_ROW_DMA=1 (measurement): the next row's remaining groups by LDS-DMA before the stores */
-        const char *edma = getenv("HSFFT_ROW_DMA");
-        const bool dma = f45 && edma && atoi(edma) != 0;
-        size_t lds = lds0;
-        if (dma) {
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, true>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, true>;
-            using DR = DmaRuns<3, 3, P, 512, 1>;
-            lds = (size_t)NT * sizeof(double2) + (size_t)DR::NRUN * DR::PITCH * sizeof(double2);
-        }
-        /* non-temporal row stores measured slower: 6.32 vs 5.96 ms (round 4, removed) */
+        /* measured slower and removed (round 4): non-temporal row stores 6.32 vs 5.96 ms; the
+         * next row's remaining groups copied into LDS by LDS-DMA before this row's stores, 6.15
+         * vs 5.94 (the load wait moves into the store phase: profiles/r04n_c3_dma_*) */
         const int threads = 512;
         int ncu = 0, dev = 0;
         HCHK(hipGetDevice(&dev));
