@@ -1116,15 +1116,6 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
         /* [8,8,8,8] first pass (2^21 = r2c 2^22's inner pass A): 32-B paired loads, one column
          * per thread group, L = 512 twiddles from global memory */
         const int q = env("HSFFT_PFP", 4);
-        if (q > 0 && env("HSFFT_PFP_G", 1) == 2 && p->A % 4 == 0 && !l->conj) {
-            /* measurement: 64-B row segments (two 2-column tiles, 1024 threads: one workgroup
-             * per CU), non-temporal stores */
-            *G = 4;
-            *TL = q;
-            *threads = 1024;
-            *lds = (size_t)4096 * 2 * sizeof(double) + 511 * sizeof(double2);
-            return l->sgn == 1 ? k_firstq<8, 3, 2, 1, false, true> : k_firstq<8, 3, 2, -1, false, true>;
-        }
         if (q > 0) {
             *G = 2; /* columns per tile group, for the grid */
             *TL = q;

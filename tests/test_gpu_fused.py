@@ -107,13 +107,11 @@ def test_paired_load_first_pass_2p21(pfp, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("nt,g", [("0", "1"), ("1", "1"), ("1", "2")])
-def test_paired_load_first_pass_2p21_nt_stores(nt, g, monkeypatch):
-    """the same pass with plain / non-temporal (default) output stores (HSFFT_PFA_NT bit 0), and
-    its 64-B-segment form (HSFFT_PFP_G=2: two 2-column tiles, 1024 threads): bit-exact, both
-    signs"""
+@pytest.mark.parametrize("nt", ["0", "1"])
+def test_paired_load_first_pass_2p21_nt_stores(nt, monkeypatch):
+    """the same pass with plain / non-temporal (default) output stores (HSFFT_PFA_NT bit 0):
+    bit-exact, both signs"""
     monkeypatch.setenv("HSFFT_PFA_NT", nt)
-    monkeypatch.setenv("HSFFT_PFP_G", g)
     n = 1 << 21
     x = T.complex_input(n, 0x2121, batch=3).reshape(3, n)
     for sgn in (1, -1):
