@@ -604,7 +604,7 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 }
 
 /* stages 4 (radix 7) and 5 (radix 8) of the pair's group, then the row's stores */
-template <int P, int TPG, bool CONJ>
+template <int P, int TPG, bool CONJ, int TWN = 0>
 __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const double2 *ltw, const double2 *tw,
                                              double2 *out, int jt, int sgn)
 {
@@ -631,6 +631,9 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
      * d = 3 is idle), k = g + jj*G45.  Per step the pair swaps 4 values: A sends output 4 + d of
      * its butterflies (B's inputs 0..3), B sends output d of its butterflies (A's inputs 4..7) */
     const double2 *twb = tw + (L5 - 1);
+    /* TWN: step d+1's stage-5 twiddles are loaded before step d's stores, so waiting for them
+     * does not wait for those stores (vmcnt counts loads and stores in issue order) */
+    double2 tn[7]; /* step 0 loads its own (no store precedes it) */
 #pragma unroll
     for (int d = 0; d < 4; d++) {
         const int jj = h ? 4 + d : d, da = d < 3 ? 4 + d : 6;
@@ -647,8 +650,16 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
         const unsigned k = g + (unsigned)(h && d == 3 ? 0 : jj) * G45; /* B's d = 3 is idle: a valid k */
 #pragma unroll
         for (int i = 1; i < 8; i++) {
-            const double2 t = pf::ldg(twb, (7 * k + i - 1) * 16u);
+            /* TWN 2 (timing probe, development builds): constant twiddles, results wrong */
+            const double2 t = TWN == 2 ? make_double2(0.5, 0.25 * i) : TWN == 1 && d > 0 ? tn[i - 1] : pf::ldg(twb, (7 * k + i - 1) * 16u);
             hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
+        }
+        if constexpr (TWN == 1) { /* after the products (the current run is dead), before the stores */
+            if (d < 3) {
+                const unsigned kn = g + (unsigned)(h && d + 1 == 3 ? 0 : (h ? 5 + d : d + 1)) * G45;
+#pragma unroll
+                for (int i = 1; i < 8; i++) tn[i - 1] = pf::ldg(twb, (7 * kn + i - 1) * 16u);
+            }
         }
         hsb::bfly<8>(zr, zi, sgn, false);
         if (live && (h == 0 || d < 3)) {
@@ -743,7 +754,7 @@ constexpr int ROW_PRE_PTS = 8448;
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false, bool F45 = false>
+          bool F23 = false, bool F45 = false, int TWN = 0>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
@@ -841,7 +852,7 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
             mark(a, tp, 3);
-            fused45_pair<P, TPG, CONJ>(xr, xi, ltw, a.tw, out, jt, sgn);
+            fused45_pair<P, TPG, CONJ, TWN>(xr, xi, ltw, a.tw, out, jt, sgn);
             mark(a, tp, 6);
             if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + 7] += 1;
             continue;
@@ -1009,6 +1020,14 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         if (f45)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true>;
+        /* HSFFT_ROW_TWN=1 (measurement): F45's stage-5 twiddles one step ahead of the stores */
+        const char *etwn = getenv("HSFFT_ROW_TWN");
+        if (f45 && etwn && atoi(etwn) == 1)
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 1>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 1>;
+#ifdef HSFFT_DEV_PROBES
+        if (f45 && etwn && atoi(etwn) == 2 && !a.conj) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 2>;
+#endif
         /* measured slower and removed (round 4): non-temporal row stores 6.32 vs 5.96 ms; the
          * next row's remaining groups copied into LDS by LDS-DMA before this row's stores, 6.15
          * vs 5.94 (the load wait moves into the store phase: profiles/r04n_c3_dma_*) */
