@@ -603,10 +603,43 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
         for (int i = 0; i < 7; i++) x[c * 7 + i] = ld[(4 * h + c + 8 * i) * G45 + g];
 }
 
+/* TWN 3: the stage-5 twiddles of steps d >= 1 (k-blocks jj = 1, 2, 3 of thread A and 5, 6 of
+ * thread B, 225 k x 7 each) are copied into LDS before the first store of the row -- four blocks
+ * into the free exchange image, the fifth behind the stage twiddle copy -- transposed to
+ * [i-1][k - 225 jj]; step 0 reads its run from global as before (no store precedes it).  So no
+ * twiddle load waits behind a store burst (vmcnt is in order). */
+constexpr int F45_BLK = 1575; /* 225 k x 7 entries */
+__device__ __forceinline__ const double2 *f45_slot(const double2 *img, const double2 *extra, int s)
+{
+    return s < 4 ? img + s * F45_BLK : extra;
+}
+template <int P, int TPG>
+__device__ __forceinline__ void f45_tw_copy(const double2 *tw, double2 *img, double2 *extra, int jt)
+{
+    constexpr int G45 = P / 56, L5 = 7 * G45, NE = 5 * F45_BLK, NIT = (NE + TPG - 1) / TPG;
+    static_assert(G45 * 7 == F45_BLK, "F45 block");
+    double2 v[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; it++) {
+        int e = it * TPG + jt;
+        if (e >= NE) e = NE - 1;
+        const int blk = e / F45_BLK, r = e % F45_BLK, jj = blk < 3 ? blk + 1 : blk + 2;
+        v[it] = pf::ldg(tw, (unsigned)(L5 - 1 + 7 * G45 * jj + r) * 16u);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; it++) {
+        const int e = it * TPG + jt;
+        if (e >= NE) continue;
+        const int blk = e / F45_BLK, r = e % F45_BLK;
+        const_cast<double2 *>(f45_slot(img, extra, blk))[(r % 7) * G45 + r / 7] = v[it];
+    }
+}
+
 /* stages 4 (radix 7) and 5 (radix 8) of the pair's group, then the row's stores */
 template <int P, int TPG, bool CONJ, int TWN = 0>
 __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const double2 *ltw, const double2 *tw,
-                                             double2 *out, int jt, int sgn)
+                                             double2 *out, int jt, int sgn, const double2 *timg = nullptr,
+                                             const double2 *textra = nullptr)
 {
     constexpr int G45 = P / 56, L4 = G45, L5 = 7 * G45;
     const int h = jt & 1, g0 = jt >> 1;
@@ -631,9 +664,6 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
      * d = 3 is idle), k = g + jj*G45.  Per step the pair swaps 4 values: A sends output 4 + d of
      * its butterflies (B's inputs 0..3), B sends output d of its butterflies (A's inputs 4..7) */
     const double2 *twb = tw + (L5 - 1);
-    /* TWN: step d+1's stage-5 twiddles are loaded before step d's stores, so waiting for them
-     * does not wait for those stores (vmcnt counts loads and stores in issue order) */
-    double2 tn[7]; /* step 0 loads its own (no store precedes it) */
 #pragma unroll
     for (int d = 0; d < 4; d++) {
         const int jj = h ? 4 + d : d, da = d < 3 ? 4 + d : 6;
@@ -651,15 +681,14 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
 #pragma unroll
         for (int i = 1; i < 8; i++) {
             /* TWN 2 (timing probe, development builds): constant twiddles, results wrong */
-            const double2 t = TWN == 2 ? make_double2(0.5, 0.25 * i) : TWN == 1 && d > 0 ? tn[i - 1] : pf::ldg(twb, (7 * k + i - 1) * 16u);
+            double2 t;
+            if constexpr (TWN == 2) t = make_double2(0.5, 0.25 * i);
+            else if constexpr (TWN == 3) {
+                /* slots 0-2: A's d = 1..3; 3, 4: B's d = 1, 2 (B's idle d = 3 reads slot 2) */
+                const int sl = h ? (d == 3 ? 2 : d + 2) : d - 1;
+                t = d == 0 ? pf::ldg(twb, (7 * k + i - 1) * 16u) : f45_slot(timg, textra, sl)[(i - 1) * G45 + g];
+            } else t = pf::ldg(twb, (7 * k + i - 1) * 16u);
             hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
-        }
-        if constexpr (TWN == 1) { /* after the products (the current run is dead), before the stores */
-            if (d < 3) {
-                const unsigned kn = g + (unsigned)(h && d + 1 == 3 ? 0 : (h ? 5 + d : d + 1)) * G45;
-#pragma unroll
-                for (int i = 1; i < 8; i++) tn[i - 1] = pf::ldg(twb, (7 * kn + i - 1) * 16u);
-            }
         }
         hsb::bfly<8>(zr, zi, sgn, false);
         if (live && (h == 0 || d < 3)) {
@@ -852,7 +881,13 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
             xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
             mark(a, tp, 3);
-            fused45_pair<P, TPG, CONJ, TWN>(xr, xi, ltw, a.tw, out, jt, sgn);
+            if constexpr (TWN == 3) {
+                __syncthreads(); /* every wave has read the image */
+                f45_tw_copy<P, TPG>(a.tw, reinterpret_cast<double2 *>(img), ltw + NT, jt);
+                __syncthreads();
+            }
+            fused45_pair<P, TPG, CONJ, TWN>(xr, xi, ltw, a.tw, out, jt, sgn, reinterpret_cast<const double2 *>(img),
+                                            ltw + NT);
             mark(a, tp, 6);
             if (a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + 7] += 1;
             continue;
@@ -994,7 +1029,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
     }
     if (v->row) { /* 12600 = [3,3,5,5,7,8]: k_row2 (the only whole-row variant) */
         constexpr int P = 12600, NT = 1574;
-        const size_t lds = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
+        const size_t lds0 = (size_t)P * sizeof(double) + (size_t)NT * sizeof(double2);
         if (l->batch <= 0) {
             snprintf(g_err, sizeof g_err, "mr: bad row batch=%d", l->batch);
             return -1;
@@ -1020,14 +1055,20 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         if (f45)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true>;
-        /* HSFFT_ROW_TWN=1 (measurement): F45's stage-5 twiddles one step ahead of the stores */
+        /* HSFFT_ROW_TWN (measurement): 3 F45's stage-5 twiddles of steps 1-3 copied into LDS
+         * before the row's stores; 2 (development builds, results wrong) constant twiddles.
+         * Loading step d+1's run before step d's stores in registers spills 17 dwords: 7.01 vs
+         * 5.93 ms (round 4, removed) */
         const char *etwn = getenv("HSFFT_ROW_TWN");
-        if (f45 && etwn && atoi(etwn) == 1)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 1>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 1>;
 #ifdef HSFFT_DEV_PROBES
         if (f45 && etwn && atoi(etwn) == 2 && !a.conj) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 2>;
 #endif
+        size_t lds = lds0;
+        if (f45 && etwn && atoi(etwn) == 3) { /* stage-5 twiddles of steps 1-3 through LDS */
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 3>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 3>;
+            lds = lds0 + (size_t)F45_BLK * sizeof(double2);
+        }
         /* measured slower and removed (round 4): non-temporal row stores 6.32 vs 5.96 ms; the
          * next row's remaining groups copied into LDS by LDS-DMA before this row's stores, 6.15
          * vs 5.94 (the load wait moves into the store phase: profiles/r04n_c3_dma_*) */
