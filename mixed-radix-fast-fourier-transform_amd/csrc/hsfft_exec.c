@@ -583,10 +583,24 @@ static hs_devstate *devstate(hs_entry *e)
     retire_devstate(e->ds[d]); /* a concurrent small call may still hold it */
     e->ds[d] = NULL;
     hs_devstate *s = calloc(1, sizeof *s);
-    const size_t twb = sizeof(fft_data) * (size_t)(e->M > 1 ? e->M : 1);
+    /* mixed-radix plans up to 64 Ki points also get their last stage's twiddles transposed to
+     * [i-1][k] at d_tw + M (the row kernel's stage-5 reads: one 16-B word per lane, lanes on
+     * consecutive k) */
+    const int trl = e->lt == 0 && e->M > 1 && e->M <= 65536 && e->nst >= 1 && e->stage_r[e->nst - 1] > 1;
+    const size_t twb = sizeof(fft_data) * (size_t)(e->M > 1 ? e->M : 1) * (trl ? 2 : 1);
     const fft_data *twsrc = e->tw_from_struct ? e->key->twiddle : e->tw_private;
     s->d_tw = hsd_malloc(twb);
     if (!s->d_tw || hsd_h2d(s->d_tw, twsrc, sizeof(fft_data) * (size_t)(e->M > 1 ? e->M - 1 : 0))) goto fail;
+    if (trl) {
+        const int r = e->stage_r[e->nst - 1], L = e->M / r;
+        fft_data *t = malloc(sizeof(fft_data) * (size_t)(r - 1) * (size_t)L);
+        if (!t) goto fail;
+        for (int k = 0; k < L; k++)
+            for (int i = 0; i < r - 1; i++) t[(size_t)i * L + k] = twsrc[L - 1 + (r - 1) * k + i];
+        const int rc = hsd_h2d((fft_data *)s->d_tw + e->M, t, sizeof(fft_data) * (size_t)(r - 1) * (size_t)L);
+        free(t);
+        if (rc) goto fail;
+    }
     if (e->ngcs) {
         s->d_gcs = hsd_malloc(sizeof(double) * (size_t)e->ngcs);
         if (!s->d_gcs || hsd_h2d(s->d_gcs, e->gcs, sizeof(double) * (size_t)e->ngcs)) goto fail;

@@ -687,6 +687,9 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
                 /* slots 0-2: A's d = 1..3; 3, 4: B's d = 1, 2 (B's idle d = 3 reads slot 2) */
                 const int sl = h ? (d == 3 ? 2 : d + 2) : d - 1;
                 t = d == 0 ? pf::ldg(twb, (7 * k + i - 1) * 16u) : f45_slot(timg, textra, sl)[(i - 1) * G45 + g];
+            } else if constexpr (TWN == 4) {
+                /* the plan's transposed copy of this stage's block at tw + P ([i-1][k]) */
+                t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
             } else t = pf::ldg(twb, (7 * k + i - 1) * 16u);
             hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
         }
@@ -1064,6 +1067,9 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         if (f45 && etwn && atoi(etwn) == 2 && !a.conj) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 2>;
 #endif
         size_t lds = lds0;
+        if (f45 && etwn && atoi(etwn) == 4) /* stage-5 twiddles from the transposed copy */
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4>;
         if (f45 && etwn && atoi(etwn) == 3) { /* stage-5 twiddles of steps 1-3 through LDS */
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 3>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 3>;

@@ -722,7 +722,8 @@ def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
-                                 {"HSFFT_ROW_TWN": "3"}])
+                                 {"HSFFT_ROW_TWN": "3"},
+                                 {"HSFFT_ROW_TWN": "4"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -733,7 +734,8 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, stages 4-5 fused
     over thread pairs (F45), the next row's first input group prefetched into registers), the
     same with stages 4 and 5 apart, without the stage 2-3 fusion, with F45's stage-5 twiddles
-    of steps 1-3 copied into LDS per row (HSFFT_ROW_TWN=3), and the two mixed-radix passes."""
+    of steps 1-3 copied into LDS per row (HSFFT_ROW_TWN=3) or read from the plan's transposed
+    copy of that stage's block (=4), and the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600
