@@ -1055,21 +1055,26 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
                                : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true>)
                      : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1>
                                : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1>);
+        /* F45's stage-5 twiddles (default since round 4) from the plan's transposed copy of the
+         * stage's block (d_tw + P: one 16-B word per lane, lanes on consecutive k, where the
+         * table's own layout puts a lane's 7 entries 112 B from its neighbour's): 5.77 vs 5.87 ms
+         * per 65536 rows in-process (profiles/r04r_c3_stage5_transposed.txt) */
         if (f45)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true>;
-        /* HSFFT_ROW_TWN (measurement): 3 F45's stage-5 twiddles of steps 1-3 copied into LDS
-         * before the row's stores; 2 (development builds, results wrong) constant twiddles.
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4>;
+        /* HSFFT_ROW_TWN (measurement): 0 stage-5 twiddles from the table as laid out; 3 those of
+         * steps 1-3 copied into LDS before the row's stores (6.20 vs 5.89 ms); 2 (development
+         * builds, results wrong) constant twiddles (5.46-5.49: what the twiddle loads cost).
          * Loading step d+1's run before step d's stores in registers spills 17 dwords: 7.01 vs
-         * 5.93 ms (round 4, removed) */
+         * 5.93 ms (removed) */
         const char *etwn = getenv("HSFFT_ROW_TWN");
+        if (f45 && etwn && atoi(etwn) == 0)
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 0>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 0>;
 #ifdef HSFFT_DEV_PROBES
         if (f45 && etwn && atoi(etwn) == 2 && !a.conj) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 2>;
 #endif
         size_t lds = lds0;
-        if (f45 && etwn && atoi(etwn) == 4) /* stage-5 twiddles from the transposed copy */
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4>;
         if (f45 && etwn && atoi(etwn) == 3) { /* stage-5 twiddles of steps 1-3 through LDS */
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 3>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 3>;

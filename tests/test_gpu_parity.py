@@ -723,7 +723,7 @@ def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
                                  {"HSFFT_ROW_TWN": "3"},
-                                 {"HSFFT_ROW_TWN": "4"}])
+                                 {"HSFFT_ROW_TWN": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -732,10 +732,11 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     exactly ONE row, so no row can lean on an earlier row's barriers (the stage-1 twiddles of
     the fused first stages are read right after the per-workgroup LDS copy).  Schedules:
     mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, stages 4-5 fused
-    over thread pairs (F45), the next row's first input group prefetched into registers), the
-    same with stages 4 and 5 apart, without the stage 2-3 fusion, with F45's stage-5 twiddles
-    of steps 1-3 copied into LDS per row (HSFFT_ROW_TWN=3) or read from the plan's transposed
-    copy of that stage's block (=4), and the two mixed-radix passes."""
+    over thread pairs (F45) with the stage-5 twiddles from the plan's transposed copy of that
+    stage's block, the next row's first input group prefetched into registers), the same with
+    stages 4 and 5 apart, without the stage 2-3 fusion, with F45's stage-5 twiddles of steps
+    1-3 copied into LDS per row (HSFFT_ROW_TWN=3) or read from the table as laid out (=0), and
+    the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600
