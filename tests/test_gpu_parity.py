@@ -721,6 +721,48 @@ def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_12600_row_kernel_edited_twiddles_refresh(monkeypatch):
+    """The row kernel reads the last stage's twiddles from a transposed copy that the device
+    state builds beside the plan's table: after the caller edits the plan's public twiddle
+    table (last-stage and stage-4 entries) and calls hsfft_plan_refresh, the default schedule
+    must use the edited values -- bit-equal to the two mixed-radix passes (which read the table
+    as laid out) and to the row kernel reading the table directly, and different from the
+    unedited transform"""
+    import ctypes
+    n, rows = 12600, 40
+    x = T.complex_input(n, 91, batch=rows).reshape(rows, n)
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    d0, d1, d2, d3 = (hsfft.DeviceBuffer(x.nbytes) for _ in range(4))
+    hsfft.exec_batched(p, din, d0, rows)  # unedited, device state built
+    hsfft.synchronize()
+    tw = (ctypes.c_double * (2 * (n - 1))).from_address(p.ptr + hsfft.STRUCT_TWIDDLE_OFFSET)
+    L5, L4 = n // 8, n // 56
+    for e in list(range(L5 - 1, L5 - 1 + 7 * 40)) + list(range(n - 200, n - 1)) + list(range(L4 - 1, L4 + 60)):
+        tw[2 * e] *= 0.75      # real part
+        tw[2 * e + 1] += 0.125  # imaginary part
+    hsfft.check(hsfft.lib().hsfft_plan_refresh(hsfft.VP(p.ptr)), "refresh")
+    hsfft.exec_batched(p, din, d1, rows)  # default: transposed copy of the edited table
+    hsfft.synchronize()
+    monkeypatch.setenv("HSFFT_MR_ROW", "0")
+    hsfft.exec_batched(p, din, d2, rows)
+    hsfft.synchronize()
+    monkeypatch.delenv("HSFFT_MR_ROW")
+    monkeypatch.setenv("HSFFT_ROW_TWN", "0")
+    hsfft.exec_batched(p, din, d3, rows)
+    hsfft.synchronize()
+    monkeypatch.delenv("HSFFT_ROW_TWN")
+    y0, y1, y2, y3 = (d.to_array(np.complex128).reshape(rows, n) for d in (d0, d1, d2, d3))
+    assert T.bits_equal(y1, y2)
+    assert T.bits_equal(y1, y3)
+    assert not np.array_equal(y0, y1)
+    assert T.bits_equal(y0, T.oracle_c2c(x, 1))
+    for d in (din, d0, d1, d2, d3):
+        d.free()
+    p.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
                                  {"HSFFT_ROW_TWN": "3"},
                                  {"HSFFT_ROW_TWN": "0"}])
