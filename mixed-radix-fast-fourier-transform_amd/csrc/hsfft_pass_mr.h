@@ -786,7 +786,7 @@ constexpr int ROW_PRE_PTS = 8448;
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false, bool F45 = false, int TWN = 0, bool PFE = false>
+          bool F23 = false, bool F45 = false, int TWN = 0>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
@@ -846,10 +846,6 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
                 r8::pin(*reinterpret_cast<double(*)[8]>(xr));
                 mark(a, tp, 0); /* loads + stages 0-1 */
             }
-            if constexpr (PF > 0 && PFE) { /* PFE: the next row's first groups before the exchange */
-                const unsigned bn = b + gridDim.x < (unsigned)a.batch ? b + gridDim.x : b;
-                f01_load0<R0, R1, P, TPG, PF>(p0, a.in + (long long)bn * a.idist, jt);
-            }
             if constexpr (F23) {
                 xchg1_f01_ab<R0, R1, R2, R3, P, TPG>(xr, img, jt);
                 xchg1_f01_ab<R0, R1, R2, R3, P, TPG>(xi, img, jt);
@@ -857,7 +853,7 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
                 xchg1_f01<R0, R1, R2, P, TPG>(xr, img, jt);
                 xchg1_f01<R0, R1, R2, P, TPG>(xi, img, jt);
             }
-            if constexpr (PF > 0 && !PFE) { /* unconditional: the last row of a workgroup reloads itself */
+            if constexpr (PF > 0) { /* unconditional: the last row of a workgroup reloads itself */
                 const unsigned bn = b + gridDim.x < (unsigned)a.batch ? b + gridDim.x : b;
                 f01_load0<R0, R1, P, TPG, PF>(p0, a.in + (long long)bn * a.idist, jt);
             }
@@ -1072,10 +1068,8 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * Loading step d+1's run before step d's stores in registers spills 17 dwords: 7.01 vs
          * 5.93 ms (removed) */
         const char *etwn = getenv("HSFFT_ROW_TWN");
-        const char *epfe = getenv("HSFFT_ROW_PFE"); /* measurement: PF loads before the first exchange */
-        if (f45 && epfe && atoi(epfe) != 0)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4, true>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4, true>;
+        /* the next row's first group loaded before this row's first exchange instead of after
+         * it: 6.11 vs 5.98 ms (round 4, removed) */
         if (f45 && etwn && atoi(etwn) == 0)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 0>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 0>;

@@ -765,8 +765,7 @@ def test_12600_row_kernel_edited_twiddles_refresh(monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
                                  {"HSFFT_ROW_TWN": "3"},
-                                 {"HSFFT_ROW_TWN": "0"},
-                                 {"HSFFT_ROW_PFE": "1"}])
+                                 {"HSFFT_ROW_TWN": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
 def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
@@ -778,9 +777,8 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     over thread pairs (F45) with the stage-5 twiddles from the plan's transposed copy of that
     stage's block, the next row's first input group prefetched into registers), the same with
     stages 4 and 5 apart, without the stage 2-3 fusion, with F45's stage-5 twiddles of steps
-    1-3 copied into LDS per row (HSFFT_ROW_TWN=3) or read from the table as laid out (=0), with
-    the next row's first group loaded before the first exchange (HSFFT_ROW_PFE=1), and the two
-    mixed-radix passes."""
+    1-3 copied into LDS per row (HSFFT_ROW_TWN=3) or read from the table as laid out (=0), and
+    the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600

@@ -39,10 +39,10 @@ BUDGETS = [
     # 12600 row kernel (c3, default since round 4: stages 4-5 fused over thread pairs,
     # HSFFT_ROW_F45=1, stage-5 twiddles from the transposed copy, HSFFT_ROW_TWN=4; the other
     # twiddle variants beside it): one 512-thread workgroup per CU
-    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb1ELi4ELb0EE", 0, 256, 2),
-    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb1ELi[034]ELb[01]EE", 0, 256, 2),
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb1ELi4EE", 0, 256, 2),
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb1ELi[03]EE", 0, 256, 2),
     # the same with stages 4 and 5 apart (HSFFT_ROW_F45=0)
-    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb0ELi0ELb0EE", 0, 256, 2),
+    (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb0ELi0EE", 0, 256, 2),
     # persistent Bluestein (c4): the whole grid (2 workgroups per CU) must be resident, so
     # 128 VGPRs is a hard limit; 8 dwords of spill are intrinsic (also compiled alone)
     (r"^_ZN3bxc6k_bxcdILin?1EE", 8, 128, 4),
