@@ -798,18 +798,16 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
 /* PFH: the next tile's hi rows are loaded at the start of this tile's pairs phase, i.e. before
  * its store burst, so waiting for them does not wait for the stores (vmcnt is in order); PFL:
  * the lo rows are loaded at the start of the hi phase, while the hi tile is transformed */
-template <int SGN, bool PFH, bool PFL, int PROBE, bool PERSIST>
-__device__ __forceinline__ void walk1_item(const Args &a, unsigned h, unsigned T, unsigned W, unsigned blk,
-                                           double2 *lds)
+template <int SGN, bool PFH = false, bool PFL = false, int PROBE = 0>
+__global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
 {
     constexpr int P = 512, TPG = 64, G = 8;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *cry = lds + P * G;
     double *ld = reinterpret_cast<double *>(lds); /* [0, 4096): split image / hi imag, [4096, 8192): hi real */
-    const unsigned nb = (unsigned)a.batch;
+    const unsigned blk = xcd_remap(blockIdx.x), nb = (unsigned)a.batch;
     const unsigned b = a.tile_major ? blk % nb : blk / (W + 1), s = a.tile_major ? blk / nb : blk % (W + 1);
-    unsigned tid0 = threadIdx.x;
-    if constexpr (PERSIST) asm volatile("" : "+v"(tid0)); /* per item: nothing thread-dependent is hoisted out of the loop */
-    const unsigned B = (unsigned)a.B, N = 2 * h;
+    const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
     const double2 *row = a.in + (long long)b * a.idist;
     double2 *X = a.out + (long long)b * a.odist;
     const double2 *w2t = a.saux;
@@ -950,28 +948,6 @@ __device__ __forceinline__ void walk1_item(const Args &a, unsigned h, unsigned T
     }
 }
 
-
-/* PERSIST: a grid of two workgroups per CU that walks the same items (walks and column-0
- * tiles) in the order the hardware would dispatch them (XCD x takes its contiguous share of
- * the logical blocks, as xcd_remap assigns them), instead of one workgroup per item */
-template <int SGN, bool PFH = false, bool PFL = false, int PROBE = 0, bool PERSIST = false>
-__global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
-{
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    if constexpr (!PERSIST) {
-        walk1_item<SGN, PFH, PFL, PROBE, false>(a, h, T, W, xcd_remap(blockIdx.x), lds);
-    } else {
-        const unsigned tot = (W + 1) * (unsigned)a.batch, x = blockIdx.x % 8, per = gridDim.x / 8;
-        const unsigned q8 = tot / 8, r8_ = tot % 8;
-        const unsigned start = x < r8_ ? x * (q8 + 1) : r8_ * (q8 + 1) + (x - r8_) * q8, cnt = q8 + (x < r8_ ? 1 : 0);
-#pragma unroll 1
-        for (unsigned i = blockIdx.x / 8; i < cnt; i += per) {
-            __syncthreads(); /* the previous item's last LDS reads are done */
-            walk1_item<SGN, PFH, PFL, PROBE, true>(a, h, T, W, start + i, lds);
-        }
-    }
-}
-
 inline int env(const char *name, int dflt);
 
 /* returns 1 if not applicable, 0 on launch, < 0 on error */
@@ -1064,20 +1040,8 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
             HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 4 * sizeof(unsigned), st));
             a.dbg = s_dbg;
         }
-        long long lgrid = grid;
-        if (walk == 3 && !dbg && env("HSFFT_R2C_PERSIST", 0) == 1 && env("HSFFT_R2C_PFH", 1) == 1) {
-            /* measurement: two persistent workgroups per CU walking the items */
-            int dev = 0, ncu = 0;
-            HCHK(hipGetDevice(&dev));
-            HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            const long long pg = 2LL * (ncu > 0 ? ncu : 256) / 8 * 8;
-            if (pg >= 8 && pg < grid) {
-                fw = sgn == 1 ? k_r2c_walk1<1, true, false, 0, true> : k_r2c_walk1<-1, true, false, 0, true>;
-                lgrid = pg;
-            }
-        }
         HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
-        hipLaunchKernelGGL(fw, dim3((unsigned)lgrid), dim3(512), lds_bytes, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
+        hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), lds_bytes, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());
         if (dbg) { /* mean us per tile pair of the walking workgroups */
             unsigned *hb = (unsigned *)malloc((size_t)grid * 4 * sizeof(unsigned));

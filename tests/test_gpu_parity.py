@@ -699,36 +699,6 @@ def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,batch,wt,sgn", [(1 << 22, 64, "32", 1), (1 << 22, 61, "32", -1), (1 << 19, 67, "4", 1)])
-def test_r2c_walk1_persistent_grid(n, batch, wt, sgn, monkeypatch):
-    """HSFFT_R2C_PERSIST=1: two workgroups per CU walking the same items (walks + column-0
-    tiles; grid > 2 per CU so the loop engages, odd batches leave the XCD shares uneven) --
-    every word equal to the one-workgroup-per-item launch, sampled rows vs the oracle"""
-    monkeypatch.setenv("HSFFT_R2C_WT", wt)
-    rp = hsfft.RealPlan(n, sgn)
-    din = hsfft.DeviceBuffer(batch * n * 8)
-    hsfft.fill_real(din, batch * n, 4242)
-    nbytes = batch * n * 16
-    d1, d2 = hsfft.DeviceBuffer(nbytes), hsfft.DeviceBuffer(nbytes)
-    hsfft.fill_complex(d1, batch * n, 1)
-    hsfft.fill_complex(d2, batch * n, 2)
-    hsfft.r2c_batched(rp, din, d1, batch)
-    hsfft.synchronize()
-    monkeypatch.setenv("HSFFT_R2C_PERSIST", "1")
-    hsfft.r2c_batched(rp, din, d2, batch)
-    hsfft.synchronize()
-    monkeypatch.delenv("HSFFT_R2C_PERSIST")
-    assert hsfft.count_diff_words(d1, d2, nbytes) == 0
-    for row in (0, batch - 1):
-        y = d2.to_array(np.complex128, n, row * n * 16)
-        x = T.real_input(n, 4242, batch=1, row0=row)
-        assert T.bits_equal(y, T.oracle_r2c(x.reshape(1, n), sgn)[0]), row
-    for d in (din, d1, d2):
-        d.free()
-    rp.close()
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("n,batch,ovl", [(1 << 22, 5, 2), (1 << 17, 7, 3), (1 << 17, 4, 1)])
 def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
     """HSFFT_R2C_OVL: pass A of each sub-chunk on the library stream, the split walk on the

@@ -30,12 +30,10 @@ BUDGETS = [
     (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]ELb[01]EE", 0, 128, 4),
     # r2c split walk (c5, default since round 4: the next hi tile's rows loaded before the
     # stores, HSFFT_R2C_PFH=1): two 512-thread workgroups per CU, 128 VGPRs, no spill
-    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0ELb0EE", 0, 128, 4),
+    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0EE", 0, 128, 4),
     # its other prefetch variants: at most one dword of spill (PFH=0: reloaded where the
     # stage-2 twiddles are waited for anyway)
-    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb[01]ELb[01]ELi0ELb0EE", 1, 128, 4),
-    # the persistent-grid walk (HSFFT_R2C_PERSIST, measurement)
-    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0ELb1EE", 2, 128, 4),
+    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb[01]ELb[01]ELi0EE", 1, 128, 4),
     # the one-per-CU walk (HSFFT_R2C_WALK=2): up to 256 VGPRs
     (r"^_ZN2pf11k_r2c_walk2ILin?1E", 0, 256, 2),
     # 12600 row kernel (c3, default since round 4: stages 4-5 fused over thread pairs,
