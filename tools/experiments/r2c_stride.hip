@@ -88,6 +88,58 @@ __global__ __launch_bounds__(512, 4) void k_walk(const double2 *Z, unsigned pitc
     if (ar == (double)sink && ai == 1.5) X[t] = make_double2(ar, ai); /* never true: keeps the loads */
 }
 
+
+// stores only, tiles CW columns wide (CW * 16 B contiguous per u-row and stream): the four
+// streams of a tile pair written as 512 / (64 / CW) wave instructions of 64 / CW rows x CW entries
+template <int CW>
+__global__ __launch_bounds__(512, 4) void k_storesw(double2 *X, unsigned sink)
+{
+    extern __shared__ double2 lds[];
+    constexpr unsigned TW = TILES * 8 / CW, WW = TW / T; /* tile pairs per row at this width, walks */
+    const unsigned blk = xcd_remap(blockIdx.x), b = blk / WW, s = blk % WW;
+    const unsigned t = threadIdx.x, g = t % CW, jt = t / CW; /* 512 / CW rows per pass */
+    constexpr unsigned RPP = 512 / CW, NPASS = P / RPP;
+    double2 *Xr = X + (size_t)b * N;
+    const unsigned j0 = s * T, o = ((b % 8) * T) / 8;
+    const double2 z = make_double2((double)t, (double)sink);
+#pragma unroll 1
+    for (unsigned jr = 0; jr < T; jr++) {
+        const unsigned j = j0 + (o + jr) % T, q = CW * j, qm = B - CW * j - CW;
+        lds[t] = z;
+        __syncthreads();
+        const double2 zz = lds[t ^ 1];
+        __syncthreads();
+#pragma unroll
+        for (unsigned pp = 0; pp < NPASS; pp++) {
+            const unsigned u = jt + pp * RPP, p = u * B + q + g, m = (P - 1 - u) * B + qm + g;
+            Xr[p] = zz;
+            Xr[(size_t)H + p] = zz;
+            Xr[m] = zz;
+            Xr[(size_t)H + m] = zz;
+        }
+    }
+}
+
+template <int CW>
+float run_w(double2 *X, int rows, int reps)
+{
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const size_t lds = 80 * 1024;
+    constexpr unsigned TW = TILES * 8 / CW, WW = TW / T;
+    CK(hipFuncSetAttribute((const void *)k_storesw<CW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_storesw<CW>, dim3(WW * rows), dim3(512), lds, 0, X, 7u);
+    CK(hipGetLastError());
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k_storesw<CW>, dim3(WW * rows), dim3(512), lds, 0, X, 7u);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+}
+
 template <int MODE>
 float run(const double2 *Z, unsigned pitch, double2 *X, unsigned xpad, int rows, int reps)
 {
@@ -123,6 +175,12 @@ int main(int argc, char **argv)
     printf("rows %d: Z %.1f GB read, X %.1f GB written; ms per %d rows (walk only)\n", rows, gbz, 2 * gbz, rows);
     const unsigned pads[] = {0, 8, 16, 64, 256};
     for (int rep = 0; rep < 2; rep++) {
+        {
+            const float m8 = run_w<8>(X, rows, reps), m16 = run_w<16>(X, rows, reps), m32 = run_w<32>(X, rows, reps),
+                        m64 = run_w<64>(X, rows, reps);
+            printf("stores only, tile width  8 / 16 / 32 / 64 entries: %.3f / %.3f / %.3f / %.3f ms (%.2f / %.2f / %.2f / %.2f TB/s)\n",
+                   m8, m16, m32, m64, 2 * gbz / m8, 2 * gbz / m16, 2 * gbz / m32, 2 * gbz / m64);
+        }
         for (unsigned pad : pads) {
             const float ms = run<1>(Z, B + pad, X, 0, rows, reps);
             printf("loads only, Z pitch B + %3u        %8.3f ms  (%.2f TB/s)\n", pad, ms, gbz / ms);
