@@ -1,7 +1,6 @@
 #!/bin/bash
 # round-4 GPU session M: the r2c walk's memory pattern without arithmetic (tools/experiments/
-# r2c_stride): tile loads at the 64-KiB row stride vs padded pitches, the four output streams (also as
-# tiles 8 / 16 / 32 / 64 columns wide),
+# r2c_stride): tile loads at the 64-KiB row stride vs padded pitches, the four output streams,
 # both together
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
