@@ -210,6 +210,11 @@ int main(void)
     for (unsigned i = 0; i < sizeof sizes / sizeof sizes[0]; i++) run_c2c(sizes[i], sizes[i] > (1 << 17) ? 1 : 3);
     const int rsizes[] = {2, 8, 64, 1000, 8192, 1 << 16, 1 << 22, 2 * 99991, 12600};
     for (unsigned i = 0; i < sizeof rsizes / sizeof rsizes[0]; i++) run_real(rsizes[i], rsizes[i] > (1 << 20) ? 1 : 2);
+    /* r2c in one-row sub-chunks, pass A on the library stream and the split on the pipeline
+     * stream behind events (HSFFT_R2C_OVL) */
+    setenv("HSFFT_R2C_OVL", "1", 1);
+    run_real(1 << 22, 3);
+    unsetenv("HSFFT_R2C_OVL");
     run_conv(5, 3);
     run_conv(300, 17);
     run_conv(1000, 1000);
