@@ -805,11 +805,6 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     double2 *cry = lds + P * G;
     double *ld = reinterpret_cast<double *>(lds); /* [0, 4096): split image / hi imag, [4096, 8192): hi real */
-    /* HSFFT_R2C_STAGGER = n (measurement, carried in xcd_groups): the second 256 workgroups of
-     * the grid (a CU's second resident walk in the first dispatch round) start n x 127 x 64
-     * cycles late, so that the two walks of a CU run their phases apart */
-    if (a.xcd_groups > 0 && ((blockIdx.x >> 8) & 1))
-        for (int i = 0; i < a.xcd_groups; i++) __builtin_amdgcn_s_sleep(127);
     const unsigned blk = xcd_remap(blockIdx.x), nb = (unsigned)a.batch;
     const unsigned b = a.tile_major ? blk % nb : blk / (W + 1), s = a.tile_major ? blk / nb : blk % (W + 1);
     const unsigned tid0 = threadIdx.x, B = (unsigned)a.B, N = 2 * h;
@@ -1034,7 +1029,6 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
 #endif
         }
         a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
-        if (walk == 3) a.xcd_groups = env("HSFFT_R2C_STAGGER", 0);
         static unsigned *s_dbg = nullptr;
         static long long s_dbg_n = 0;
         if (dbg) {
