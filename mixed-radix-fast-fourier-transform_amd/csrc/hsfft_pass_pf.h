@@ -1096,11 +1096,13 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
     for (int s = 1; s < p->nst; s++)
         if (p->radix[s] != 8) return nullptr;
     if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 4) { /* 2^20's pass A: [4,8,8,8] */
-        /* k_firstq walking 4 column groups: 24.0-24.3 ms per 4096 x 2^20 against 27.0-27.2 for
-         * its 32-B-segment predecessor k_first (round 1; removed in round 3) */
+        /* k_firstq: 24.0-24.3 ms per 4096 x 2^20 against 27.0-27.2 for its 32-B-segment
+         * predecessor k_first (round 1; removed in round 3).  One column group per workgroup
+         * (HSFFT_PFQ, default 1 since round 4): in-process 46.19 / 45.86 vs 46.49 / 46.06 ms per
+         * step for walks of 4 groups on two boxes, walks of 2 47.17 (profiles/r04aa_*, r04ab_*) */
         if (p->A % 4 == 0) { /* 64-B loads: *G = 4 columns per tile for the grid */
             *G = 4;
-            *TL = env("HSFFT_PFQ", 4) > 0 ? env("HSFFT_PFQ", 4) : 4;
+            *TL = env("HSFFT_PFQ", 1) > 0 ? env("HSFFT_PFQ", 1) : 1;
             *threads = 512;
             *lds = (size_t)2048 * 2 * sizeof(double) + 2048 * sizeof(double2);
             /* non-temporal output stores (HSFFT_PFA_NT bit 1, default on since round 4): 48.42 vs
@@ -1114,8 +1116,10 @@ inline kfn pick(const hsd_pass *p, const hsd_launch *l, int *G, int *TL, int *th
     }
     if ((mask & 1) && p->B == 1 && p->leaf && p->nst == 4 && p->radix[0] == 8 && p->A % 2 == 0) {
         /* [8,8,8,8] first pass (2^21 = r2c 2^22's inner pass A): 32-B paired loads, one column
-         * per thread group, L = 512 twiddles from global memory */
-        const int q = env("HSFFT_PFP", 4);
+         * per thread group, L = 512 twiddles from global memory; one column group per workgroup
+         * (HSFFT_PFP, default 1 since round 4): c5 21.89 / 20.84 vs 22.01 / 21.04 ms per 512 rows
+         * for walks of 4 on two boxes, walks of 2 22.69 (profiles/r04aa_*, r04ab_*) */
+        const int q = env("HSFFT_PFP", 1);
         if (q > 0) {
             *G = 2; /* columns per tile group, for the grid */
             *TL = q;
