@@ -115,5 +115,11 @@ def test_no_wrong_result_probes_in_product():
     if not os.path.exists(LIB):
         pytest.skip("lib/libhsfft.so not built")
     blob = open(LIB, "rb").read()
-    for probe in (b"HSFFT_DEV_ALIAS", b"HSFFT_DEV_NPASS", b"HSFFT_R2C_PROBE", b"HSFFT_BX_PLAIN", b"HSFFT_BLUE_PROBE"):
+    for probe in (b"HSFFT_DEV_ALIAS", b"HSFFT_DEV_NPASS", b"HSFFT_R2C_PROBE", b"HSFFT_BX_PLAIN", b"HSFFT_BLUE_PROBE",
+                  b"HSFFT_R2C_W1PROBE"):
         assert probe not in blob, probe
+    # nor their kernels: k_r2c_walk1<SGN, PFH, PFL, PROBE != 0>, k_row2<..., TWN = 2> (constant twiddles)
+    names = _metadata()
+    bad = [k for k in names if re.match(r"^_ZN2pf11k_r2c_walk1ILin?1ELb[01]ELb[01]ELi[1-9]", k)
+           or re.match(r"^_ZN2mr6k_row2I.*ELi2EEEvNS_5MArgsE$", k)]
+    assert not bad, bad
