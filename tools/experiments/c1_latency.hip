@@ -8,12 +8,18 @@
 //   d) the same copy kernel followed by hipStreamWriteValue32 of a sequence number into
 //      page-locked host memory; the host polls that word (no stream wait)
 //   e) the same copy with the flag stored by the kernel itself after a system-scope fence
+//   f) as e) plus the host's memcpy of the 16 KB input into the pinned slot (the small
+//      fft_exec path's whole data movement)
+//   g) as f) but the host writes the input into fine-grained DEVICE memory (when the runtime
+//      maps it into the host's address space: large BAR), so the kernel reads HBM instead of
+//      host memory over the link
 // Build: hipcc -O2 --offload-arch=gfx950 c1_latency.hip -o c1_latency (binary git-ignored)
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
 #include <vector>
 #include <algorithm>
+#include <cstring>
 
 #define CK(x)                                                                          \
     do {                                                                               \
@@ -66,8 +72,20 @@ int main()
     CK(hipHostMalloc((void **)&hin, 16384, hipHostMallocDefault));
     CK(hipHostMalloc((void **)&hout, 16384, hipHostMallocDefault));
     for (int i = 0; i < 1024; i++) hin[i] = make_double2(i, -i);
+    std::vector<double2> user(1024);
+    for (int i = 0; i < 1024; i++) user[i] = make_double2(i, -i);
+    /* fine-grained device memory, host-mapped only if the runtime reports a host pointer */
+    double2 *dfg = nullptr, *dfg_host = nullptr;
+    if (hipExtMallocWithFlags((void **)&dfg, 16384, hipDeviceMallocFinegrained) == hipSuccess) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, dfg) == hipSuccess) dfg_host = (double2 *)at.hostPointer;
+        printf("fine-grained device buffer %p, host pointer %p\n", (void *)dfg, (void *)dfg_host);
+    } else {
+        (void)hipGetLastError();
+        printf("fine-grained device allocation refused\n");
+    }
     const int R = 2000;
-    std::vector<double> ta, tb, tc, td, te;
+    std::vector<double> ta, tb, tc, td, te, tf, tg;
     unsigned *flag2;
     CK(hipHostMalloc((void **)&flag2, 64, hipHostMallocCoherent));
     *(volatile unsigned *)flag2 = 0;
@@ -112,7 +130,36 @@ int main()
             }
         auto t8 = clk::now();
         CK(hipStreamSynchronize(st));
+        auto t9 = clk::now();
+        memcpy(hin, user.data(), 16384);
+        hipLaunchKernelGGL(k_copy_flag, dim3(1), dim3(256), 0, st, (const double2 *)hin, hout, 1024,
+                           (volatile unsigned *)flag, (unsigned)(r + 2000001));
+        spins = 0;
+        while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != (unsigned)(r + 2000001))
+            if (++spins > 2000000000L) {
+                fprintf(stderr, "kernel flag (f) never arrived\n");
+                return 1;
+            }
+        auto t10 = clk::now();
+        CK(hipStreamSynchronize(st));
+        if (dfg_host) {
+            auto t11 = clk::now();
+            memcpy(dfg_host, user.data(), 16384);
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            hipLaunchKernelGGL(k_copy_flag, dim3(1), dim3(256), 0, st, (const double2 *)dfg, hout, 1024,
+                               (volatile unsigned *)flag, (unsigned)(r + 3000001));
+            spins = 0;
+            while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != (unsigned)(r + 3000001))
+                if (++spins > 2000000000L) {
+                    fprintf(stderr, "kernel flag (g) never arrived\n");
+                    return 1;
+                }
+            auto t12 = clk::now();
+            CK(hipStreamSynchronize(st));
+            if (r >= 100) tg.push_back(std::chrono::duration<double, std::micro>(t12 - t11).count());
+        }
         if (r >= 100) {
+            tf.push_back(std::chrono::duration<double, std::micro>(t10 - t9).count());
             td.push_back(std::chrono::duration<double, std::micro>(t6 - t5).count());
             te.push_back(std::chrono::duration<double, std::micro>(t8 - t7).count());
             ta.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
@@ -125,7 +172,16 @@ int main()
         return 1;
     }
     printf("median us: empty+sync %.2f | empty+host-flag poll %.2f | 16KB pinned->pinned copy kernel+sync %.2f | "
-           "copy+writeValue poll %.2f | copy with in-kernel flag poll %.2f\n",
-           med(ta), med(tb), med(tc), med(td), med(te));
+           "copy+writeValue poll %.2f | copy with in-kernel flag poll %.2f | host memcpy into the pinned slot + "
+           "that %.2f | host memcpy into host-mapped device memory + that %.2f\n",
+           med(ta), med(tb), med(tc), med(td), med(te), med(tf), tg.empty() ? -1.0 : med(tg));
+    if (dfg_host) {
+        std::vector<double2> back(1024);
+        memcpy(back.data(), hout, 16384);
+        if (back[1023].x != 1023.0) {
+            fprintf(stderr, "device-input copy check failed\n");
+            return 1;
+        }
+    }
     return 0;
 }
