@@ -2,9 +2,12 @@
 """Benchmark: batched 1D c2c FFT N=2^20 (BASELINE.json configs[1]) on MI355X.
 
 A "step" is one hsfft_exec_batched over the per-GPU batch (4096 x 2^20 complex f64, inputs
-already resident in HBM).  Multi-GPU: one process per GPU (torch.distributed.run); each rank
-transforms its own 4096 rows (weak scaling, no data-path collective -- the path shards by
-batch index); rank 0 prints one JSON line with the max-over-ranks time.
+already resident in HBM).  Multi-GPU: one process per GPU; each rank transforms its own 4096
+rows (weak scaling, no data-path collective -- the path shards by batch index); rank 0 prints
+one JSON line with the max-over-ranks time.  `bench.py --gpus N` started without a launcher
+starts the N rank processes itself (torch.distributed.run as a child process, before anything
+touches the GPU) and exits with their status; under a launcher (torch.distributed.run sets
+WORLD_SIZE) WORLD_SIZE must equal N.
 
 Other configs: --config c1 (one N=1024 fft_exec on HOST buffers: latency, next to the
 reference timed in the same run), c3 (12600 x 65536), c4 (Bluestein 99991 x 8192), c5 (r2c
@@ -82,6 +85,24 @@ class Comm:
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: N rank processes (one per GPU) under
+    torch.distributed.run, started as CHILD processes of this one -- which has not touched the
+    GPU and never replaces itself -- on 127.0.0.1; returns their exit status."""
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, env=env)
 
 
 def row_range(rank, per_rank_batch):
@@ -558,19 +579,40 @@ def main():
                          "of 2^20-sample pairs (P = 2^21); value = padded samples P x ROWS per second")
     ap.add_argument("--dry-run", action="store_true", help="multi-rank control path on the CPU oracle (tests)")
     ap.add_argument("--dump-rows", default="",
-                    help="c2c only: after the timed steps, save the first and last output row of this rank's "
-                         "shard with their global row indices to DIR/rank<r>.npz (multi-rank parity test)")
+                    help="c2c / r2c: after the timed steps, save the first and last output row of this rank's "
+                         "shard (r2c: of the step's last output chunk) with their global row indices to "
+                         "DIR/rank<r>.npz (multi-rank parity test)")
     ap.add_argument("--dry-n", type=int, default=1024)
+    ap.add_argument("--no-finalize", action="store_true",
+                    help="skip hsfft_finalize() before exit (diagnostics: the library's teardown is on by default)")
     ap.add_argument("--host-rows", type=int, default=0,
                     help="also time hsfft_exec_batched_host on this many HOST-resident rows (PCIe-inclusive "
                          "rate, reported as host_pipeline; never the headline value)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))  # before any GPU call in this process
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(--nproc-per-node must equal --gpus)")
     comm = Comm(ws)
+    try:
+        bench_main(args, comm, ws, rank, local)
+    finally:
+        if not args.dry_run and not args.no_finalize and hsfft._lib is not None:
+            # release every device object before the process exits (a pending launch error of
+            # this thread would be reported here; say so, without masking an earlier exception)
+            if hsfft.lib().hsfft_finalize() != 0:
+                print(f"bench.py: hsfft_finalize: {hsfft.lib().hsfft_last_error().decode()}", file=sys.stderr)
+        comm.close()
+
+
+def bench_main(args, comm, ws, rank, local):
     if args.dry_run:
         dry_run(args, comm, ws, rank)
-        comm.close()
         return
     L = hsfft.lib()
     ndev = hsfft.device_count()
@@ -579,11 +621,9 @@ def main():
     hsfft.check(L.hsfft_set_device(local % ndev), "set_device")
     if args.convolve:
         bench_convolve(args, comm, ws, rank)
-        comm.close()
         return
     if args.config == "c1":
         bench_c1(args, comm, ws, rank)
-        comm.close()
         return
 
     cfg = CONFIGS[args.config]
@@ -730,14 +770,20 @@ def main():
         out["roofline"]["pass_frac"] = [round(samples * bytes_per_sample / (p / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
                                         for p in pass_ms]
     # (before the copy benchmark below overwrites dout)
-    if args.dump_rows and kind == "c2c":
+    if args.dump_rows and not args.c2r:
         import numpy as np
         g0 = row_range(rank, batch)[0]
-        picks = sorted({0, batch - 1})
-        rows = np.stack([dout.to_array(np.complex128, n, r * n * 16) for r in picks])
+        if kind == "c2c":
+            picks = sorted({0, batch - 1})
+            rows = np.stack([dout.to_array(np.complex128, n, r * n * 16) for r in picks])
+        else:  # r2c: the output buffer holds the step's last chunk of rows
+            c0 = (batch - 1) // chunk * chunk
+            orow = (n // 2 + 1) if args.r2c_compact else n
+            picks = sorted({c0, batch - 1})
+            rows = np.stack([dout.to_array(np.complex128, orow, (r - c0) * orow * 16) for r in picks])
         os.makedirs(args.dump_rows, exist_ok=True)
         np.savez(os.path.join(args.dump_rows, f"rank{rank}.npz"), rows=rows,
-                 global_rows=np.array([g0 + r for r in picks]), n=n, seed=seed, world=ws)
+                 global_rows=np.array([g0 + r for r in picks]), n=n, seed=seed, world=ws, kind=kind)
     # practical HBM ceiling on this device: a 16-B-per-lane stream copy of the same buffers
     nbytes = min(din.nbytes, dout.nbytes) // 16 * 16
     cms = hsfft.bench_copy(din, dout, nbytes, 5)
@@ -765,7 +811,6 @@ def main():
         print(json.dumps(out), flush=True)
     din.free()
     dout.free()
-    comm.close()
 
 
 if __name__ == "__main__":

@@ -43,6 +43,15 @@ int hsfft_synchronize(void);
  * HSFFT_CHUNK_MB, default 256 MiB x 2; Bluestein HSFFT_BLUE_CHUNK_MB, 4 GiB x 2; real paths
  * HSFFT_REAL_CHUNK_MB, 16 GiB -- each halved while allocation fails). */
 int hsfft_release_scratch(void);
+/* Teardown: waits for every device's work, then releases every device object the library
+ * holds on every device -- scratch pool, page-locked staging slots, the device state of every
+ * live plan (twiddles, odd-radix constants, Bluestein chirp / hk), real plans' device twiddles,
+ * idle convolution plans, persistent-launch counters and the calling thread's error words (a
+ * pending launch error of the calling thread is reported as by hsfft_synchronize), timing and
+ * ordering events, the library streams.  Plans stay valid and everything is re-created on
+ * demand, so the library remains usable.  Call it before process exit (bench.py and the test
+ * session do), with no other library call running.  Returns 0 or a negative code. */
+int hsfft_finalize(void);
 void *hsfft_get_stream(void);            /* hipStream_t of the current device */
 const char *hsfft_last_error(void);
 
@@ -103,13 +112,20 @@ int hsfft_count_diff_words(const void *d_a, const void *d_b, size_t bytes, uint6
 int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, float *ms);
 
 /* Bluestein M = 2^18 (e.g. N = 99991) runs as one persistent launch whose workgroups must all
- * be resident at once; it is launched cooperatively, so the runtime refuses a grid that cannot
- * be co-resident and the rows run on the three-launch path at once (same results, more time).
- * Count of such calls in this process.  The launch is asynchronous like every batched call;
- * its in-launch waits keep a last-resort bound (~1.3 s without progress), and a wait that
- * still times out makes the next hsfft_synchronize() return HSFFT_ERR_DEVICE (the Bluestein
- * outputs since the previous synchronisation are invalid).  HSFFT_BX_SYNC=1: each Bluestein
- * call is synchronous and re-runs the rows of a timed-out launch itself. */
+ * be resident at once; the library checks that with the occupancy API before launching, and a
+ * grid that cannot be co-resident runs on the three-launch path at once (same results, more
+ * time).  Its in-launch waits keep a last-resort bound (~1.3 s without progress):
+ *   - synchronous entry points (fft_exec, fft_r2c_exec / fft_c2r_exec, hsfft_exec_batched_host,
+ *     hsfft_exec_multi) wait for the launch and re-run the rows of a launch whose waits timed
+ *     out on the three-launch path themselves;
+ *   - asynchronous device-buffer calls (hsfft_exec_batched, hsfft_r2c_batched, ...) record a
+ *     timed-out wait in an error word of the CALLING THREAD; it is reported exactly once, as
+ *     HSFFT_ERR_DEVICE, by that thread's next hsfft_synchronize() on that device (or its next
+ *     timing call, hsfft_time_*), and it means that thread's Bluestein outputs since its previous
+ *     hsfft_synchronize() are invalid.  No other call consumes it or reports it: not a later
+ *     call on another plan, not a scratch-pool growth, not another thread's hsfft_synchronize().
+ *   HSFFT_BX_SYNC=1 makes every Bluestein call synchronous.
+ * Count of calls whose rows ran on the three-launch path (refused grid or timed-out waits). */
 long long hsfft_bluestein_fallbacks(void);
 
 /* --- threading -------------------------------------------------------------------------

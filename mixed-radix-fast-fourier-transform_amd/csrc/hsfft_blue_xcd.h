@@ -38,9 +38,11 @@
  * launch runs two, so the acquire is back.
  *
  * Residency: every workgroup of a group waits on the others, so the whole grid must be
- * resident.  The host checks the occupancy API; if something else occupies the GPU the waits
- * time out, the kernel exits, and the host re-runs the rows through the three-launch path
- * (hsfft_exec.c run_bluestein), so a busy GPU costs time, never results.
+ * resident.  The host checks the occupancy API and refuses a grid that does not fit (its rows
+ * run on the three-launch path).  If something else occupies the GPU the waits time out, the
+ * kernel exits and sets the error word: a synchronous call re-runs the rows through the
+ * three-launch path (hsfft_exec.c run_bluestein), an asynchronous one reports the error at the
+ * caller's next hsfft_synchronize().
  *
  * Uneven-load testing: a.jitter > 0 adds a pseudo-random s_sleep (0 .. jitter-1 units of
  * ~4 us) to each workgroup before its arrive and after its wait, per phase -- results are
@@ -71,7 +73,8 @@ struct XArgs {
     double2 *img;         /* [ng][NIMG][IMG] */
     long long idist, odist;
     unsigned *cnt;        /* [ng][2] counters, CS apart */
-    unsigned *err;        /* sticky error word */
+    unsigned *err;        /* sticky error word (set on a timed-out wait; every wait gives up once it is set) */
+    unsigned long long tlimit; /* wait bound in ticks of the 100 MHz real-time counter (T_LIMIT; tests lower it) */
     unsigned batch, ng, nsig, sleep;
     unsigned jitter;      /* > 0: pseudo-random per-phase delays (uneven-load tests; results unchanged) */
     unsigned merge;       /* 1: one acquire per iteration when both counters are already complete */
@@ -134,7 +137,7 @@ __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned targ
         unsigned st = 0;
         while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             for (unsigned n = 0; n < a.sleep; n++) __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > T_LIMIT ||
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.tlimit ||
                 __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 st = 1;

@@ -131,6 +131,23 @@ static void conv_plans_done(conv_pair cp)
     pthread_mutex_unlock(&g_clock);
 }
 
+/* (hsfft_finalize) free every idle cached plan pair; slots in use or being built are kept */
+void hs_conv_cache_release(void)
+{
+    fft_real_object fr[2 * HS_CONV_CACHE];
+    int n = 0;
+    pthread_mutex_lock(&g_clock);
+    for (int k = 0; k < HS_CONV_CACHE; k++)
+        if (g_cache[k].refs == 0 && !g_cache[k].building && g_cache[k].f) {
+            fr[n++] = g_cache[k].f;
+            fr[n++] = g_cache[k].i;
+            g_cache[k].f = g_cache[k].i = NULL;
+            g_cache[k].P = 0;
+        }
+    pthread_mutex_unlock(&g_clock);
+    for (int k = 0; k < n; k++) free_real_fft(fr[k]);
+}
+
 /* output window of the reference (convolve.c:163-201); returns length or -1 */
 static int conv_window(const char *type, int linear, int clen, int P, int n, int m, int *start)
 {

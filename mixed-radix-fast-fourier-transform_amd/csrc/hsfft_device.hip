@@ -642,36 +642,84 @@ int hsd_memset_async(void *d, int v, size_t bytes)
     return 0;
 }
 
-/* persistent-launch state per device (bxc::k_bxcd): a counter block (per-group counters, the
- * sticky error word) and a pinned host copy of the error word */
+/* persistent-launch state per device (bxc::k_bxcd): a counter block (2 counters per group, each
+ * on its own 128-B line), zeroed on the launch's stream before every launch */
 static unsigned *g_pl_ctr[HS_MAX_DEV];
 static size_t g_pl_bytes[HS_MAX_DEV];
-static unsigned *g_pl_err_host[HS_MAX_DEV];
 
-/* The sticky error word of the persistent launches since the last check (set on the device
- * when an in-launch wait timed out; copied to the pinned host word behind every launch, on the
- * launch's stream).  Called after a synchronisation of that stream: reports the error once and
- * clears both copies. */
-static int pl_check(void)
+/* Error words of the persistent launches, per THREAD and device: a device block whose word 0
+ * (the asynchronous sticky word) and word 32 (the synchronous call's word) a launch sets when one
+ * of its in-launch waits timed out, and a page-locked host copy of both, refreshed on the
+ * launch's stream behind every launch.  The asynchronous word is cumulative: it is read and
+ * cleared only by hsd_sync_report() of the thread that launched (hsfft_synchronize, the timing
+ * calls), so no other synchronisation -- a scratch pool growing, a device state being built, an
+ * unrelated plan's call, another thread -- can consume or inherit it.  The synchronous word is
+ * cleared before every synchronous launch and read right after it (hsd_blue_xcd returns 2). */
+struct PlErr {
+    unsigned *dev;  /* 64 words on the device: [0] async sticky, [32] sync */
+    unsigned *host; /* 64 page-locked words: copies of the same */
+};
+static thread_local PlErr t_pl[HS_MAX_DEV];
+
+static int pl_words(int dev, PlErr **out)
+{
+    PlErr *p = &t_pl[dev];
+    if (!p->dev) {
+        HCHK(hipMalloc((void **)&p->dev, 64 * sizeof(unsigned)));
+        if (hipMemset(p->dev, 0, 64 * sizeof(unsigned)) != hipSuccess ||
+            hipHostMalloc((void **)&p->host, 64 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
+            const hipError_t e = hipGetLastError();
+            (void)hipFree(p->dev);
+            p->dev = nullptr;
+            return set_err(e, "persistent-launch error words");
+        }
+        memset(p->host, 0, 64 * sizeof(unsigned));
+    }
+    *out = p;
+    return 0;
+}
+
+static void pl_release_thread(int dev)
+{
+    PlErr *p = &t_pl[dev];
+    if (p->dev) (void)hipFree(p->dev);
+    if (p->host) (void)hipHostFree(p->host);
+    p->dev = nullptr;
+    p->host = nullptr;
+}
+
+/* Report (once) a timed-out wait of this thread's asynchronous persistent launches on the
+ * current device.  Called after the library stream was synchronised, so the host copy is
+ * final. */
+static int pl_report(void)
 {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV || !g_pl_err_host[dev]) return 0;
-    if (*(volatile unsigned *)g_pl_err_host[dev] == 0) return 0;
-    *g_pl_err_host[dev] = 0;
-    if (g_pl_ctr[dev]) {
-        (void)hipMemsetAsync(g_pl_ctr[dev] + 8, 0, sizeof(unsigned), primary());
-        (void)hipStreamSynchronize(primary());
-    }
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) return 0;
+    PlErr *p = &t_pl[dev];
+    if (!p->host || *(volatile unsigned *)p->host == 0) return 0;
+    const unsigned w = *(volatile unsigned *)p->host;
+    *(volatile unsigned *)p->host = 0;
+    (void)hipMemsetAsync(p->dev, 0, sizeof(unsigned), primary());
+    (void)hipStreamSynchronize(primary());
     snprintf(g_err, sizeof g_err,
-             "persistent Bluestein launch: an in-launch dependency wait timed out; the outputs of the Bluestein "
-             "calls since the last synchronisation are invalid (HSFFT_BX_SYNC=1 re-runs such rows automatically)");
+             "persistent Bluestein launch: an in-launch dependency wait timed out (error word %u); the outputs of this "
+             "thread's Bluestein calls since its last hsfft_synchronize() on this device are invalid "
+             "(HSFFT_BX_SYNC=1 re-runs such rows automatically)", w);
     return -2;
 }
 
+/* wait for the library stream; a pending persistent-launch error stays pending */
 int hsd_sync(void)
 {
     HCHK(hipStreamSynchronize(primary()));
-    return pl_check();
+    return 0;
+}
+
+/* the same, and report this thread's pending persistent-launch error (hsfft_synchronize) */
+int hsd_sync_report(void)
+{
+    HCHK(hipStreamSynchronize(primary()));
+    return pl_report();
 }
 
 /* wait for the library stream by polling an event (no blocking wait / wake-up): for short
@@ -694,21 +742,24 @@ int hsd_sync_spin(void)
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) return set_err(e, "hipEventQuery");
     }
-    return pl_check();
+    return 0;
 }
 
 /* Bluestein M = 2^18 as one persistent launch (hsfft_blue_xcd.h).  img: ng x 4 x M points of
- * scratch.  The grid is launched COOPERATIVELY (hipLaunchCooperativeKernel): the runtime
- * checks at launch that every workgroup can be resident at once and refuses the launch
- * otherwise (returned as 1: the caller runs the three-launch path at once).
- * Asynchronous by default: the launch is queued on the library stream with a copy of its sticky
- * error word behind it; a wait that still timed out (the last-resort bound, ~1.3 s without
- * progress) is reported by the next hsfft_synchronize().  HSFFT_BX_SYNC=1: synchronous, and a
+ * scratch.  Every workgroup must be resident at once: the occupancy API is asked on the host
+ * and a grid that does not fit is refused (returned as 3: the caller runs the three-launch
+ * path at once).  HSFFT_BX_COOP=1 launches through hipLaunchCooperativeKernel instead, which
+ * makes the runtime do the same check (round 4's default; DESIGN.md §5 round 5 for why it is
+ * not the default any more).
+ * Asynchronous (sync == 0): the launch is queued on the library stream with a copy of this
+ * thread's sticky error word behind it; a wait that still timed out (the last-resort bound,
+ * ~1.3 s without progress; HSFFT_BX_TLIMIT ticks of the 100 MHz counter for tests) is reported
+ * by this thread's next hsd_sync_report().  Synchronous (sync != 0): the call waits, and a
  * timed-out launch returns 2 so the caller re-runs its rows on the three-launch path.
- * Returns 0 on success (queued), 1 if not applicable, 2 (sync mode) if an in-launch wait timed
- * out, 3 if the cooperative launch was refused, < 0 on a HIP error. */
+ * Returns 0 on success (queued), 1 if not applicable, 2 (sync) if an in-launch wait timed out,
+ * 3 if the grid cannot be co-resident, < 0 on a HIP error. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
-                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng)
+                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng, int sync)
 {
     int dev = 0;
     HCHK(hipGetDevice(&dev));
@@ -719,31 +770,41 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     void (*fn)(bxc::XArgs) = sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>;
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bxc::LDS_BYTES));
     const int grid = ng * (int)bxc::NTILE;
-    /* counter block: [0, 32) the sticky error word (word 8) on its own line, then 2 counters
-     * per group, each on a 128-B line; the counters are zeroed before every launch (Guideline
-     * 16, re-initialise every call), the error word only when it is reported (pl_check) */
+    const char *ce = getenv("HSFFT_BX_COOP");
+    const bool coop = ce && atoi(ce);
+    if (!coop) { /* co-residency: workgroups per CU the occupancy API allows x CUs */
+        int per_cu = 0, ncu = 0;
+        HCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, 512, bxc::LDS_BYTES));
+        HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        if ((long long)per_cu * ncu < grid) {
+            snprintf(g_err, sizeof g_err, "hsd_blue_xcd: %d workgroups cannot be co-resident (%d per CU x %d CUs)", grid,
+                     per_cu, ncu);
+            return 3;
+        }
+    }
+    PlErr *pe = nullptr;
+    {
+        const int rc = pl_words(dev, &pe);
+        if (rc) return rc;
+    }
     const size_t CS = bxc::CS;
-    const size_t need = (CS + 2 * CS * (size_t)ng) * sizeof(unsigned);
+    const size_t need = 2 * CS * (size_t)ng * sizeof(unsigned);
     if (g_pl_bytes[dev] < need) {
         if (g_pl_ctr[dev]) {
-            HCHK(hipStreamSynchronize(stream()));
-            const int rc = pl_check(); /* do not lose a pending error word */
+            HCHK(hipStreamSynchronize(stream())); /* an earlier launch may still use the block */
             HCHK(hipFree(g_pl_ctr[dev]));
             g_pl_ctr[dev] = nullptr;
             g_pl_bytes[dev] = 0;
-            if (rc) return rc;
         }
         const size_t alloc = (need + 4095) & ~(size_t)4095;
         HCHK(hipMalloc((void **)&g_pl_ctr[dev], alloc));
-        HCHK(hipMemset(g_pl_ctr[dev], 0, alloc));
         g_pl_bytes[dev] = alloc;
-        if (!g_pl_err_host[dev]) {
-            HCHK(hipHostMalloc((void **)&g_pl_err_host[dev], 64, hipHostMallocDefault));
-            *g_pl_err_host[dev] = 0;
-        }
     }
     unsigned *ctr = g_pl_ctr[dev];
-    HCHK(hipMemsetAsync(ctr + CS, 0, need - CS * sizeof(unsigned), stream()));
+    /* the counters are zeroed before every launch (Guideline 16, re-initialise every call) */
+    HCHK(hipMemsetAsync(ctr, 0, need, stream()));
+    unsigned *err = sync ? pe->dev + 32 : pe->dev;
+    if (sync) HCHK(hipMemsetAsync(err, 0, sizeof(unsigned), stream()));
     bxc::XArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)in;
@@ -754,12 +815,12 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     a.img = (double2 *)img;
     a.idist = idist;
     a.odist = odist;
-    a.cnt = ctr + CS;
-    a.err = ctr + 8;
+    a.cnt = ctr;
+    a.err = err;
     a.batch = (unsigned)batch;
     a.ng = (unsigned)ng;
     a.nsig = (unsigned)nsig;
-    bool sync_mode = false;
+    a.tlimit = bxc::T_LIMIT;
     {
         const char *e = getenv("HSFFT_BX_SLEEP");
         a.sleep = e ? (unsigned)atoi(e) : 1u;
@@ -771,39 +832,47 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
          * measured slower (c4 23.6-23.7 vs 24.3-24.5 GSamples/s with one acquire per wait) */
         e = getenv("HSFFT_BX_MERGE");
         a.merge = e ? (unsigned)atoi(e) & 1u : 0u;
-        e = getenv("HSFFT_BX_SYNC");
-        sync_mode = e && atoi(e);
+        e = getenv("HSFFT_BX_TLIMIT"); /* tests: force the timeout path (ticks of 10 ns) */
+        if (e && atoll(e) > 0) a.tlimit = (unsigned long long)atoll(e);
     }
-    static unsigned *s_dbg = nullptr;
+    static unsigned *s_dbg[HS_MAX_DEV];
     const char *dbgenv = getenv("HSFFT_BX_DEBUG");
     const bool dbg = dbgenv && atoi(dbgenv) && grid <= 4096;
     if (dbg) {
-        if (!s_dbg) HCHK(hipMalloc((void **)&s_dbg, 4096 * 8 * sizeof(unsigned)));
-        HCHK(hipMemsetAsync(s_dbg, 0, (size_t)grid * 8 * sizeof(unsigned), stream()));
-        a.dbg = s_dbg;
-        sync_mode = true;
+        if (!s_dbg[dev]) HCHK(hipMalloc((void **)&s_dbg[dev], 4096 * 8 * sizeof(unsigned)));
+        HCHK(hipMemsetAsync(s_dbg[dev], 0, (size_t)grid * 8 * sizeof(unsigned), stream()));
+        a.dbg = s_dbg[dev];
+        sync = 1;
     }
-    void *kargs[] = {&a};
-    const hipError_t le = hipLaunchCooperativeKernel((const void *)fn, dim3((unsigned)grid), dim3(512), kargs,
-                                                     (unsigned)bxc::LDS_BYTES, stream());
-    if (le != hipSuccess) {
-        (void)hipGetLastError();
-        if (le == hipErrorCooperativeLaunchTooLarge) {
-            snprintf(g_err, sizeof g_err, "hsd_blue_xcd: cooperative launch of %d workgroups refused (not co-resident)", grid);
-            return 3; /* refused at launch: the caller runs the three-launch path */
+    if (coop) {
+        void *kargs[] = {&a};
+        const hipError_t le = hipLaunchCooperativeKernel((const void *)fn, dim3((unsigned)grid), dim3(512), kargs,
+                                                         (unsigned)bxc::LDS_BYTES, stream());
+        if (le != hipSuccess) {
+            (void)hipGetLastError();
+            if (le == hipErrorCooperativeLaunchTooLarge) {
+                snprintf(g_err, sizeof g_err, "hsd_blue_xcd: cooperative launch of %d workgroups refused (not co-resident)",
+                         grid);
+                return 3; /* refused at launch: the caller runs the three-launch path */
+            }
+            return set_err(le, "hipLaunchCooperativeKernel(k_bxcd)");
         }
-        return set_err(le, "hipLaunchCooperativeKernel(k_bxcd)");
+    } else {
+        hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
+        HCHK(hipGetLastError());
     }
-    HCHK(hipMemcpyAsync(g_pl_err_host[dev], ctr + 8, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
-    if (!sync_mode) return 0;
+    /* host copy of the word this launch could set (async: the cumulative sticky word) */
+    unsigned *hw = sync ? pe->host + 32 : pe->host;
+    HCHK(hipMemcpyAsync(hw, err, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
+    if (!sync) return 0;
     HCHK(hipStreamSynchronize(stream()));
-    const unsigned err = *(volatile unsigned *)g_pl_err_host[dev];
+    const unsigned w = *(volatile unsigned *)hw;
     if (dbg) { /* mean us per row: P1, wait A, P2, wait B, P3 */
         static unsigned h[4096 * 8];
-        HCHK(hipMemcpy(h, s_dbg, (size_t)grid * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
+        HCHK(hipMemcpy(h, s_dbg[dev], (size_t)grid * 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
         double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int w = 0; w < grid; w++)
-            for (int i = 0; i < 8; i++) t[i] += h[w * 8 + i];
+        for (int wg = 0; wg < grid; wg++)
+            for (int i = 0; i < 8; i++) t[i] += h[wg * 8 + i];
         const double rows = t[0] > 0 ? t[0] : 1;
         fprintf(stderr,
                 "bxcd: wgs %d rows/wg %.1f  us per row: P1 %.2f (+drain %.2f) waitA %.2f P2 %.2f (+drain %.2f) waitB %.2f "
@@ -811,20 +880,22 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
                 grid, t[0] / grid, t[1] / rows / 100.0, t[6] / rows / 100.0, t[2] / rows / 100.0, t[3] / rows / 100.0,
                 t[7] / rows / 100.0, t[4] / rows / 100.0, t[5] / rows / 100.0);
     }
-    if (err) { /* sync mode: consume the word here (the caller re-runs the rows) */
-        *g_pl_err_host[dev] = 0;
-        HCHK(hipMemsetAsync(ctr + 8, 0, sizeof(unsigned), stream()));
-        HCHK(hipStreamSynchronize(stream()));
-        snprintf(g_err, sizeof g_err, "hsd_blue_xcd: an in-launch wait timed out (error word %u)", err);
+    if (w) { /* the caller re-runs the rows */
+        *(volatile unsigned *)hw = 0;
+        snprintf(g_err, sizeof g_err, "hsd_blue_xcd: an in-launch wait timed out (error word %u)", w);
         return 2;
     }
     return 0;
 }
 
+/* differing 8-byte words; the counter is one per-device word kept for the process */
+static unsigned long long *g_diff_word[HS_MAX_DEV];
+
 int hsd_count_diff(const void *a, const void *b, long long nwords, unsigned long long *count)
 {
-    unsigned long long *d = nullptr;
-    HCHK(hipMalloc((void **)&d, sizeof *d));
+    const int dev = cur_dev();
+    if (!g_diff_word[dev]) HCHK(hipMalloc((void **)&g_diff_word[dev], sizeof(unsigned long long)));
+    unsigned long long *d = g_diff_word[dev];
     HCHK(hipMemsetAsync(d, 0, sizeof *d, stream()));
     if (nwords > 0)
         hipLaunchKernelGGL(k_count_diff, dim3(8192), dim3(256), 0, stream(), (const unsigned long long *)a,
@@ -832,7 +903,6 @@ int hsd_count_diff(const void *a, const void *b, long long nwords, unsigned long
     HCHK(hipGetLastError());
     HCHK(hipMemcpyAsync(count, d, sizeof *d, hipMemcpyDeviceToHost, stream()));
     HCHK(hipStreamSynchronize(stream()));
-    HCHK(hipFree(d));
     return 0;
 }
 
@@ -856,8 +926,61 @@ void hsd_thread_release(void)
             (void)hipEventDestroy(t_spin_ev[d]);
             t_spin_have[d] = false;
         }
+        pl_release_thread(d);
     }
     (void)hipGetLastError();
+}
+
+/* Releases every device object this layer holds on the current device (after waiting for its
+ * streams): the persistent-launch counters, the calling thread's error words (a pending error
+ * is reported first, as hsd_sync_report would), the diff counter, the debug trace block, the
+ * timing and ordering events, the library's streams and the calling thread's own stream.  All
+ * of them are re-created on demand.  Returns the pending error or the first HIP error. */
+int hsd_finalize_device(void)
+{
+    const int dev = cur_dev();
+    int rc = 0;
+    hipStream_t *tabs[3] = {g_stream, g_stream2, g_stream3};
+    std::atomic<bool> *flags[3] = {g_stream_init, g_stream2_init, g_stream3_init};
+    for (int s = 0; s < 3; s++)
+        if (flags[s][dev].load(std::memory_order_acquire) && tabs[s][dev] &&
+            hipStreamSynchronize(tabs[s][dev]) != hipSuccess && !rc)
+            rc = set_err(hipGetLastError(), "hipStreamSynchronize");
+    if (!rc) rc = pl_report();
+    pl_release_thread(dev);
+    if (t_own[dev]) {
+        (void)hipStreamSynchronize(t_own[dev]);
+        (void)hipStreamDestroy(t_own[dev]);
+        t_own[dev] = 0;
+    }
+    if (t_spin_have[dev]) {
+        (void)hipEventDestroy(t_spin_ev[dev]);
+        t_spin_have[dev] = false;
+    }
+    std::lock_guard<std::mutex> g(g_init_mtx);
+    if (g_pl_ctr[dev]) (void)hipFree(g_pl_ctr[dev]);
+    g_pl_ctr[dev] = nullptr;
+    g_pl_bytes[dev] = 0;
+    if (g_diff_word[dev]) (void)hipFree(g_diff_word[dev]);
+    g_diff_word[dev] = nullptr;
+    if (g_ev_init[dev].load(std::memory_order_acquire)) {
+        for (int k = 0; k < HS_NEV; k++) (void)hipEventDestroy(g_ev[dev][k]);
+        g_ev_init[dev].store(false, std::memory_order_release);
+    }
+    if (g_timer_init[dev].load(std::memory_order_acquire)) {
+        (void)hipEventDestroy(g_t0[dev]);
+        (void)hipEventDestroy(g_t1[dev]);
+        for (int k = 0; k < 2 * HS_MAX_PASSES; k++) (void)hipEventDestroy(g_pev[dev][k]);
+        g_timer_init[dev].store(false, std::memory_order_release);
+    }
+    for (int s = 0; s < 3; s++)
+        if (flags[s][dev].load(std::memory_order_acquire)) {
+            if (tabs[s][dev]) (void)hipStreamDestroy(tabs[s][dev]);
+            tabs[s][dev] = 0;
+            flags[s][dev].store(false, std::memory_order_release);
+        }
+    (void)hipGetLastError();
+    return rc;
 }
 
 int hsd_select_stream(int idx)
@@ -1315,7 +1438,7 @@ int hsd_timer_stop(float *ms)
     HCHK(hipEventRecord(g_t1[dev], stream()));
     HCHK(hipEventSynchronize(g_t1[dev]));
     HCHK(hipEventElapsedTime(ms, g_t0[dev], g_t1[dev]));
-    return pl_check(); /* a timed persistent launch whose waits timed out is an error, not a time */
+    return pl_report(); /* a timed persistent launch whose waits timed out is an error, not a time */
 }
 
 int hsd_pass_timer_begin(int i)
@@ -1341,7 +1464,7 @@ int hsd_pass_timer_read(int n, float *ms)
         HCHK(hipEventSynchronize(g_pev[dev][2 * i + 1]));
         HCHK(hipEventElapsedTime(&ms[i], g_pev[dev][2 * i], g_pev[dev][2 * i + 1]));
     }
-    return pl_check();
+    return pl_report();
 }
 
 }  // extern "C"

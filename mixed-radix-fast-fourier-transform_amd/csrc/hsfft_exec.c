@@ -10,10 +10,16 @@
 #define _GNU_SOURCE
 #include <math.h>
 #include <pthread.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
 #include <stdarg.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <ucontext.h>
+#include <unistd.h>
 
 #include "hsfft_gpu.h"
 #include "hsfft_host.h"
@@ -21,6 +27,14 @@
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* the plan registry */
 static hs_entry *g_entries;
 static __thread char g_errbuf[512];
+
+/* > 0 while this thread is inside a synchronous entry point (fft_exec, the drop-in real and
+ * convolution calls, hsfft_exec_batched_host, hsfft_exec_multi's shards): the persistent
+ * Bluestein launch then runs synchronously and re-runs the rows of a timed-out launch itself,
+ * instead of leaving the error for a later hsfft_synchronize() */
+static __thread int t_sync_call;
+
+void hs_sync_call(int enter) { t_sync_call += enter ? 1 : -1; }
 
 /* per-device API locks (recursive: public entry points call each other) */
 static pthread_mutex_t g_dev_mtx[HS_MAX_DEV];
@@ -547,6 +561,138 @@ int hsfft_release_scratch(void)
     return rc;
 }
 
+static void thread_resources_free(void *unused);
+void hs_crash_trace_install(void);
+static void *g_pin[HS_MAX_DEV][2];
+static size_t g_pin_sz[HS_MAX_DEV];
+
+/* Teardown (include/hsfft_gpu.h): every device object the library holds, on every device,
+ * after waiting for that device's work -- the scratch pool, the page-locked staging slots, the
+ * device state of every live plan (twiddles, odd-radix constants, Bluestein chirp / hk), the
+ * real plans' device twiddles, the idle convolution plan pairs, the persistent-launch counters
+ * and error words, the calling thread's own slots / words / streams, the timing and ordering
+ * events and the library streams.  Everything is re-created on demand.  Callers must not run
+ * other library calls concurrently. */
+int hsfft_finalize(void)
+{
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    const int cur = hsd_get_device();
+    hs_conv_cache_release(); /* frees plans: their device state on every device goes with them */
+    thread_resources_free(NULL);
+    const int ndev = hsd_device_count() < HS_MAX_DEV ? hsd_device_count() : HS_MAX_DEV;
+    for (int d = 0; d < ndev; d++) {
+        if (hsd_set_device(d)) {
+            if (!rc) rc = HSFFT_ERR_DEVICE;
+            continue;
+        }
+        const int dl = hs_lock_device();
+        if (hsd_sync() && !rc) rc = HSFFT_ERR_DEVICE;
+        for (int c = 0; c < HS_NSCRATCH; c++) {
+            hsd_free(g_scr[d][c]);
+            g_scr[d][c] = NULL;
+            g_scr_sz[d][c] = 0;
+        }
+        hsd_host_free(g_pin[d][0]);
+        hsd_host_free(g_pin[d][1]);
+        g_pin[d][0] = g_pin[d][1] = NULL;
+        g_pin_sz[d] = 0;
+        pthread_mutex_lock(&g_lock);
+        for (hs_entry *e = g_entries; e; e = e->next)
+            if (e->ds[d]) {
+                retire_devstate(e->ds[d]);
+                e->ds[d] = NULL;
+            }
+        pthread_mutex_unlock(&g_lock);
+        hs_real_release_device(d);
+        const int fr = hsd_finalize_device();
+        if (fr && !rc) {
+            hs_seterr("hsfft_finalize: %s", hsd_errstr());
+            rc = HSFFT_ERR_DEVICE;
+        }
+        hs_unlock_device(dl);
+    }
+    if (cur >= 0) hsd_set_device(cur);
+    return rc;
+}
+
+/* HSFFT_CRASH_TRACE=1 (diagnostics): on SIGSEGV / SIGBUS / SIGILL / SIGFPE / SIGABRT the
+ * library writes the signal, the faulting address and instruction pointer, the native
+ * backtrace (library + offset per frame) and /proc/self/maps to stderr, then re-raises the
+ * signal with its default action.  Installed when the library is loaded and again when a
+ * device is selected (a tool that installs its own handler while the runtime initialises would
+ * otherwise replace it). */
+static void crash_puts(const char *s)
+{
+    size_t n = strlen(s);
+    while (n > 0) {
+        const ssize_t w = write(2, s, n);
+        if (w <= 0) return;
+        s += w;
+        n -= (size_t)w;
+    }
+}
+
+static void crash_hex(const char *label, unsigned long long v)
+{
+    char b[40];
+    int i = 39;
+    b[i] = 0;
+    do {
+        b[--i] = "0123456789abcdef"[v & 15];
+        v >>= 4;
+    } while (v && i > 2);
+    b[--i] = 'x';
+    b[--i] = '0';
+    crash_puts(label);
+    crash_puts(b + i);
+}
+
+static void crash_handler(int sig, siginfo_t *si, void *ucv)
+{
+    crash_hex("\n*** hsfft crash trace: signal ", (unsigned long long)sig);
+    crash_hex(" fault address ", (unsigned long long)(uintptr_t)si->si_addr);
+#if defined(__x86_64__)
+    const ucontext_t *uc = (const ucontext_t *)ucv;
+    crash_hex(" rip ", (unsigned long long)uc->uc_mcontext.gregs[REG_RIP]);
+#else
+    (void)ucv;
+#endif
+    crash_puts("\n*** backtrace:\n");
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, n, 2);
+    crash_puts("*** /proc/self/maps:\n");
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        char buf[4096];
+        ssize_t r;
+        while ((r = read(fd, buf, sizeof buf)) > 0)
+            if (write(2, buf, (size_t)r) != r) break;
+        close(fd);
+    }
+    crash_puts("*** end of hsfft crash trace\n");
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+void hs_crash_trace_install(void)
+{
+    const char *e = getenv("HSFFT_CRASH_TRACE");
+    if (!e || !atoi(e)) return;
+    void *warm[2];
+    (void)backtrace(warm, 2); /* loads the unwinder now, not inside the handler */
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = crash_handler;
+    sa.sa_flags = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    const int sigs[] = {SIGSEGV, SIGBUS, SIGILL, SIGFPE, SIGABRT};
+    for (unsigned i = 0; i < sizeof sigs / sizeof sigs[0]; i++) sigaction(sigs[i], &sa, NULL);
+}
+
+__attribute__((constructor)) static void crash_trace_ctor(void) { hs_crash_trace_install(); }
+
 /* Chunk sizes, one knob per path, all read per call: HSFFT_CHUNK_MB (c2c intermediates of
  * 3+-pass chains), HSFFT_BLUE_CHUNK_MB (Bluestein M-point intermediates), HSFFT_REAL_CHUNK_MB
  * (the real paths' inner intermediate, hsfft_real.c). */
@@ -583,10 +729,13 @@ static hs_devstate *devstate(hs_entry *e)
     retire_devstate(e->ds[d]); /* a concurrent small call may still hold it */
     e->ds[d] = NULL;
     hs_devstate *s = calloc(1, sizeof *s);
-    /* mixed-radix plans up to 64 Ki points also get their last stage's twiddles transposed to
-     * [i-1][k] at d_tw + M (the row kernel's stage-5 reads: one 16-B word per lane, lanes on
-     * consecutive k) */
-    const int trl = e->lt == 0 && e->M > 1 && e->M <= 65536 && e->nst >= 1 && e->stage_r[e->nst - 1] > 1;
+    /* the one schedule whose kernel reads it -- the whole-row [3,3,5,5,7,8] pass (12600, the
+     * mr::k_row2 F45 kernel) -- also gets its last stage's twiddles transposed to [i-1][k] at
+     * d_tw + M (one 16-B word per lane, lanes on consecutive k); the launch is told by
+     * hsd_launch.tw_t, so no other kernel can read an unbuilt region */
+    static const int row_r[6] = {3, 3, 5, 5, 7, 8};
+    int trl = e->lt == 0 && e->npass == 1 && e->pass[0].variant == HS_KV_MR && e->pass[0].nst == 6;
+    for (int i = 0; trl && i < 6; i++) trl = e->pass[0].radix[i] == row_r[i];
     const size_t twb = sizeof(fft_data) * (size_t)(e->M > 1 ? e->M : 1) * (trl ? 2 : 1);
     const fft_data *twsrc = e->tw_from_struct ? e->key->twiddle : e->tw_private;
     s->d_tw = hsd_malloc(twb);
@@ -632,6 +781,7 @@ static hs_devstate *devstate(hs_entry *e)
         e->ds[d] = NULL;
         if (rc) goto fail;
     }
+    s->tw_t = trl;
     e->ds[d] = s;
     e->ds_version[d] = ver;
     return s;
@@ -669,6 +819,7 @@ static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long
     l.dir = dir;
     l.conj = conj;
     l.tw = ds->d_tw;
+    l.tw_t = ds->tw_t;
     l.gcs = (const double *)ds->d_gcs;
     l.load_op = load_op;
     l.load_aux = laux;
@@ -798,8 +949,9 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
     return 0;
 }
 
-/* persistent Bluestein launches whose rows ran on the three-launch path instead (cooperative
- * launch refused, or waits timed out in HSFFT_BX_SYNC=1 mode); hsfft_bluestein_fallbacks() */
+/* persistent Bluestein launches whose rows ran on the three-launch path instead (grid not
+ * co-resident, or waits timed out in a synchronous call); hsfft_bluestein_fallbacks() */
+static void thread_resources_used(void);
 static long long g_blue_fallbacks;
 
 long long hsfft_bluestein_fallbacks(void) { return __atomic_load_n(&g_blue_fallbacks, __ATOMIC_RELAXED); }
@@ -822,20 +974,24 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
                      p0->radix[0] == 8 && !env_int("HSFFT_BLUE_NOFUSE", 0);
     /* one persistent launch per 65536 rows (hsfft_blue_xcd.h): groups of 64 workgroups carry
      * one row at a time through all three kernels, the intermediates stay on die
-     * (HSFFT_BLUE_XCD=0: three launches per chunk).  The launch is cooperative: if its grid
-     * cannot be co-resident the runtime refuses it and the rows run on the three-launch path
-     * below at once.  Asynchronous; in HSFFT_BX_SYNC=1 mode a launch whose waits timed out
-     * makes its rows run on the three-launch path as well.  Both count as fallbacks. */
+     * (HSFFT_BLUE_XCD=0: three launches per chunk).  A grid that cannot be co-resident is
+     * refused on the host and its rows run on the three-launch path below at once.  Device-
+     * buffer batched calls are asynchronous (a timed-out wait is reported by the caller's next
+     * hsfft_synchronize()); synchronous entry points (t_sync_call) and HSFFT_BX_SYNC=1 wait,
+     * and a launch whose waits timed out makes its rows run on the three-launch path as well.
+     * Both count as fallbacks. */
     const int ng = env_int("HSFFT_BLUE_XCD", 8);
+    const int sync = t_sync_call > 0 || env_int("HSFFT_BX_SYNC", 0);
     long long done = 0;
     if (fuse && ng > 0) {
+        thread_resources_used(); /* this thread's error words are freed when it exits */
         const size_t ib = (size_t)ng * 4 * sizeof(fft_data) * (size_t)M; /* 4 images per group */
         void *img = hs_scratch(3, ib);
         int rc = img ? 0 : 1;
         for (long long c0 = 0; c0 < batch && rc == 0; c0 += 65536) {
             const int cb = (int)(batch - c0 < 65536 ? batch - c0 : 65536);
             rc = hsd_blue_xcd((const fft_data *)in + c0 * idist, idist, (fft_data *)out + c0 * odist, odist, ds->d_tw,
-                              ds->d_chirp, ds->d_hk, img, ib, N, cb, e->sgn, ng);
+                              ds->d_chirp, ds->d_hk, img, ib, N, cb, e->sgn, ng, sync);
             if (rc == 0) done = c0 + cb;
         }
         if (rc < 0) {
@@ -965,9 +1121,6 @@ int hs_c2c_rows(hs_entry *e, const void *in, long long idist, void *out, long lo
  * rows are copied into page-locked host slots and the kernel reads and writes them over the
  * host link directly -- no H2D / D2H copy launches, one kernel launch and one wait per call
  * (BASELINE config 1, N = 1024).  Per-device slots, used under the device lock. */
-static void *g_pin[HS_MAX_DEV][2];
-static size_t g_pin_sz[HS_MAX_DEV];
-
 static int small_host_exec(hs_entry *e, const fft_data *inp, fft_data *oup, size_t bytes)
 {
     const int d = hsd_get_device();
@@ -1001,6 +1154,7 @@ static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
     if (hs_require_gpu()) fatal("fft_exec needs an MI355X");
     hs_entry *e = hs_entry_get(obj);
     if (!e) fatal("fft_exec: invalid plan");
+    t_sync_call++;
     const int N = obj->N;
     const size_t bytes = sizeof(fft_data) * (size_t)N;
     const int din = hsd_is_device_ptr(inp), dout = hsd_is_device_ptr(oup);
@@ -1020,6 +1174,7 @@ static void fft_exec_locked(fft_object obj, fft_data *inp, fft_data *oup)
         if (!rc) rc = dout ? hsd_d2d_async(oup, dq, bytes) : hsd_d2h(oup, dq, bytes);
     }
     if (!rc) rc = hsd_sync();
+    t_sync_call--;
     hs_entry_put(e);
     if (rc) fatal("fft_exec failed");
 }
@@ -1148,14 +1303,19 @@ void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
 
 /* ------------------------------------------------------------------ extension API */
 int hsfft_device_count(void) { return hsd_device_count(); }
-int hsfft_set_device(int dev) { return hsd_set_device(dev) ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_set_device(int dev)
+{
+    const int rc = hsd_set_device(dev) ? HSFFT_ERR_DEVICE : 0;
+    hs_crash_trace_install(); /* after the runtime (and any tool) initialised: ours wins */
+    return rc;
+}
 int hsfft_get_device(void) { return hsd_get_device(); }
 void *hsfft_malloc(size_t bytes) { return hs_require_gpu() ? NULL : hsd_malloc(bytes); }
 int hsfft_free(void *p) { return hsd_free(p) ? HSFFT_ERR_DEVICE : 0; }
 int hsfft_memcpy_h2d(void *d, const void *h, size_t n) { return hsd_h2d(d, h, n) ? HSFFT_ERR_DEVICE : 0; }
 int hsfft_memcpy_d2h(void *h, const void *d, size_t n) { return hsd_d2h(h, d, n) ? HSFFT_ERR_DEVICE : 0; }
 int hsfft_memset(void *d, int v, size_t n) { return hsd_memset_async(d, v, n) ? HSFFT_ERR_DEVICE : 0; }
-int hsfft_synchronize(void) { return hsd_sync() ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_synchronize(void) { return hsd_sync_report() ? HSFFT_ERR_DEVICE : 0; }
 void *hsfft_get_stream(void) { return hsd_stream(); }
 
 int hsfft_plan_refresh(fft_object obj)
@@ -1239,7 +1399,9 @@ int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_ou
     if (rc) return rc;
     const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(obj);
+    t_sync_call++;
     rc = e ? exec_host_locked(obj, e, h_in, h_out, batch) : HSFFT_ERR_ARG;
+    t_sync_call--;
     hs_entry_put(e);
     hs_unlock_device(d);
     return rc;
@@ -1395,8 +1557,10 @@ static void *shard_main(void *arg)
 {
     hs_shard *s = arg;
     s->rc = hsd_set_device(s->dev) ? HSFFT_ERR_DEVICE : 0;
+    t_sync_call++; /* the shard waits anyway: Bluestein rows of a timed-out launch are re-run */
     if (!s->rc && s->rows > 0) s->rc = hsfft_exec_batched(s->obj, s->in, s->out, s->rows);
-    if (!s->rc && hsd_sync()) s->rc = HSFFT_ERR_DEVICE;
+    if (!s->rc && hsd_sync_report()) s->rc = HSFFT_ERR_DEVICE;
+    t_sync_call--;
     if (s->rc) snprintf(s->err, sizeof s->err, "device %d: %.400s", s->dev, g_errbuf[0] ? g_errbuf : hsd_errstr());
     return NULL;
 }

@@ -19,6 +19,7 @@ typedef struct hs_devstate {
     void *d_gcs;  /* odd-radix cos/sin constants */
     void *d_chirp;/* Bluestein chirp h(n), N complex */
     void *d_hk;   /* Bluestein spectrum of the scaled, mirrored chirp, M complex */
+    int tw_t;     /* 1: d_tw + M holds the last stage's block transposed (the 12600 row kernel) */
     /* users outside the device lock (the concurrent small fft_exec path) pin the state for
      * their whole call: a rebuild (hsfft_plan_refresh) then retires it instead of freeing it,
      * and the last hs_devstate_put frees it.  Both fields change under the device lock. */
@@ -81,6 +82,13 @@ int hs_c2r_rows(fft_real_object r, const fft_data *d_in, long long xdist, fft_ty
 int hs_c2r_product_rows(fft_real_object r, const fft_data *d_a, const fft_data *d_b, long long xdist, fft_type *d_out,
                         int batch);
 void *hs_scratch(int cls, size_t bytes);
+/* brackets a synchronous entry point on this thread (1 enter, 0 leave): persistent Bluestein
+ * launches inside it wait and re-run timed-out rows instead of reporting them later */
+void hs_sync_call(int enter);
+/* release this layer's device objects (hsfft_finalize): idle convolution plan pairs, real
+ * plans' device twiddles on the current device */
+void hs_conv_cache_release(void);
+void hs_real_release_device(int dev);
 /* bytes from an environment knob given in MiB (default dflt_mb; at least 1 MiB) */
 size_t hs_env_mb(const char *name, double dflt_mb);
 

@@ -63,6 +63,7 @@ typedef struct {
     const void *load_aux, *store_aux;
     long long nsig;
     int nt_load, nt_store;          /* non-temporal input / output (register kernels) */
+    int tw_t;                       /* 1: tw + M holds the last stage's block transposed ([i-1][k]) */
     /* completion word (small host-buffer calls): a kernel that runs as ONE workgroup stores
      * done_val into *done (page-locked host memory) after every wave published its output at
      * system scope, and the device layer sets *armed; other launches ignore it */
@@ -81,8 +82,12 @@ int hsd_h2d(void *d, const void *h, size_t bytes);
 int hsd_d2h(void *h, const void *d, size_t bytes);
 int hsd_d2d_async(void *d, const void *s, size_t bytes);
 int hsd_memset_async(void *d, int v, size_t bytes);
-int hsd_sync(void);
-int hsd_sync_spin(void);          /* the same, polling instead of a blocking wait */
+int hsd_sync(void);               /* wait for the library stream (a pending launch error stays pending) */
+int hsd_sync_report(void);        /* the same, then report this thread's pending persistent-launch error */
+int hsd_sync_spin(void);          /* hsd_sync polling an event instead of a blocking wait */
+/* release every device object of the device layer on the current device (streams, events,
+ * persistent-launch counters, this thread's error words); re-created on demand */
+int hsd_finalize_device(void);
 int hsd_select_stream(int idx);   /* 0 library stream, 1 pipeline / H2D, 2 D2H, 3 this thread's own stream */
 int hsd_stream_index(void);       /* the calling thread's selected stream */
 int hsd_h2d_async(void *d, const void *h, size_t bytes);   /* on the selected stream */
@@ -114,12 +119,12 @@ int mr_has_variant(const hsd_pass *p);
  * h+1 bins (hsfft_r2c_batched_compact) instead of the mirrored N */
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
                  long long B, int batch, int sgn, int compact);
-/* Bluestein M = 2^18 in one persistent, cooperative launch (hsfft_blue_xcd.h), asynchronous
- * (HSFFT_BX_SYNC=1: synchronous): 0 queued / done, 1 not applicable, 2 (sync mode) in-launch
- * waits timed out, 3 cooperative launch refused (re-run the rows elsewhere in both), < 0 HIP
- * error.  In async mode a timed-out wait is reported by the next hsd_sync. */
+/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h), asynchronous unless `sync`:
+ * 0 queued / done, 1 not applicable, 2 (sync) in-launch waits timed out, 3 grid not co-resident
+ * (re-run the rows elsewhere in both), < 0 HIP error.  Asynchronous: a timed-out wait is
+ * reported by the launching thread's next hsd_sync_report. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
-                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng);
+                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng, int sync);
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
 int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
                  int conj, int dir, int sgn2, int conj2); /* hsfft_pass_mr.h has a kernel for this pass */

@@ -1059,29 +1059,31 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * stage's block (d_tw + P: one 16-B word per lane, lanes on consecutive k, where the
          * table's own layout puts a lane's 7 entries 112 B from its neighbour's): 5.77 vs 5.87 ms
          * per 65536 rows in-process (profiles/r04r_c3_stage5_transposed.txt) */
-        if (f45)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4>;
-        /* HSFFT_ROW_TWN (measurement): 0 stage-5 twiddles from the table as laid out; 3 those of
-         * steps 1-3 copied into LDS before the row's stores (6.20 vs 5.89 ms); 2 (development
-         * builds, results wrong) constant twiddles (5.46-5.49: what the twiddle loads cost).
-         * Loading step d+1's run before step d's stores in registers spills 17 dwords: 7.01 vs
-         * 5.93 ms (removed) */
+        /* The transposed copy exists only when the plan's device state built it (l->tw_t, set
+         * for exactly this schedule); without it the table is read as laid out (TWN 0, also
+         * HSFFT_ROW_TWN=0) */
         const char *etwn = getenv("HSFFT_ROW_TWN");
+        const bool twn4 = l->tw_t && !(etwn && atoi(etwn) == 0);
+        if (f45)
+            fn = twn4 ? (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4>
+                                : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4>)
+                      : (a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 0>
+                                : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 0>);
         /* the next row's first group loaded before this row's first exchange instead of after
          * it: 6.11 vs 5.98 ms (round 4, removed) */
-        if (f45 && etwn && atoi(etwn) == 0)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 0>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 0>;
-#ifdef HSFFT_DEV_PROBES
-        if (f45 && etwn && atoi(etwn) == 2 && !a.conj) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 2>;
-#endif
         size_t lds = lds0;
-        if (f45 && etwn && atoi(etwn) == 3) { /* stage-5 twiddles of steps 1-3 through LDS */
+#ifdef HSFFT_DEV_PROBES
+        /* development build only (measurement): HSFFT_ROW_TWN=2 constant stage-5 twiddles, results
+         * wrong (5.46-5.49 ms: what the twiddle loads cost); 3 those of steps 1-3 copied into LDS
+         * before the row's stores (6.20 vs 5.89 ms).  Loading step d+1's run before step d's
+         * stores in registers spills 17 dwords: 7.01 vs 5.93 ms (removed) */
+        if (f45 && etwn && atoi(etwn) == 2 && !a.conj) fn = k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 2>;
+        if (f45 && etwn && atoi(etwn) == 3) {
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 3>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 3>;
             lds = lds0 + (size_t)F45_BLK * sizeof(double2);
         }
+#endif
         /* measured slower and removed (round 4): non-temporal row stores 6.32 vs 5.96 ms; the
          * next row's remaining groups copied into LDS by LDS-DMA before this row's stores, 6.15
          * vs 5.94 (the load wait moves into the store phase: profiles/r04n_c3_dma_*) */

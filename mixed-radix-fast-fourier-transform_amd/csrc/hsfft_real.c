@@ -100,6 +100,18 @@ void free_real_fft(fft_real_object r)
     free(r);
 }
 
+/* (hsfft_finalize) drop every real plan's device twiddles on device `dev` (rebuilt on demand) */
+void hs_real_release_device(int dev)
+{
+    pthread_mutex_lock(&g_rlock);
+    for (hs_real_entry *e = g_real; e; e = e->next)
+        if (e->d_tw2[dev]) {
+            hsd_free(e->d_tw2[dev]);
+            e->d_tw2[dev] = NULL;
+        }
+    pthread_mutex_unlock(&g_rlock);
+}
+
 /* row chunk for the inner c2c's intermediate Z (scratch class 4): HSFFT_CHUNK_MB of Z per
  * chunk, default 16 GiB (measured, 4096 x 2^22 r2c, fused split: 2 GiB 91.7, 4 GiB 94.1,
  * 8 GiB 98.3, 16 GiB 99.9 GSamples/s -- longer launches fill the chip better); halved while
@@ -310,7 +322,9 @@ static void r2c_exec_locked(fft_real_object r, fft_type *inp, fft_data *oup)
 void fft_r2c_exec(fft_real_object r, fft_type *inp, fft_data *oup)
 {
     const int d = hs_lock_device();
+    hs_sync_call(1); /* synchronous: a Bluestein inner plan re-runs timed-out rows itself */
     r2c_exec_locked(r, inp, oup);
+    hs_sync_call(0);
     hs_unlock_device(d);
 }
 
@@ -343,6 +357,8 @@ static void c2r_exec_locked(fft_real_object r, fft_data *inp, fft_type *oup)
 void fft_c2r_exec(fft_real_object r, fft_data *inp, fft_type *oup)
 {
     const int d = hs_lock_device();
+    hs_sync_call(1); /* synchronous: a Bluestein inner plan re-runs timed-out rows itself */
     c2r_exec_locked(r, inp, oup);
+    hs_sync_call(0);
     hs_unlock_device(d);
 }

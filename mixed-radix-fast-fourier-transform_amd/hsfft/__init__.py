@@ -46,6 +46,7 @@ SIGNATURES = {
     "hsfft_memset": (CI, [VP, CI, ctypes.c_size_t]),
     "hsfft_synchronize": (CI, []),
     "hsfft_release_scratch": (CI, []),
+    "hsfft_finalize": (CI, []),
     "hsfft_get_stream": (VP, []),
     "hsfft_last_error": (ctypes.c_char_p, []),
     "hsfft_set_twiddle_mode": (CI, [CI]),
@@ -69,6 +70,8 @@ SIGNATURES = {
     "hsfft_bluestein_fallbacks": (ctypes.c_longlong, []),
     "hsfft_count_diff_words": (CI, [VP, VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]),
 }
+
+HSFFT_ERR_ARG, HSFFT_ERR_DEVICE, HSFFT_ERR_NOMEM = -1, -2, -3  # include/hsfft_gpu.h
 
 STRUCT_TWIDDLE_OFFSET = 272  # offsetof(struct fft_set, twiddle), include/highspeedFFT.h
 
@@ -264,6 +267,11 @@ def fill_real(d, count, seed, offset=0):
 
 def synchronize():
     return check(lib().hsfft_synchronize(), "synchronize")
+
+
+def finalize():
+    """hsfft_finalize(): release every device object the library holds (before process exit)"""
+    return check(lib().hsfft_finalize(), "finalize")
 
 
 def set_twiddle_mode(mode):

@@ -11,6 +11,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long CPU test")
 
 
+def pytest_sessionfinish(session, exitstatus):
+    """hsfft_finalize() before the test process exits, where the library was loaded and a GPU is
+    present: every device object the library holds is released while the runtime is intact"""
+    mod = sys.modules.get("hsfft")
+    if mod is None or getattr(mod, "_lib", None) is None:
+        return
+    try:
+        if mod.device_count() > 0:
+            mod.lib().hsfft_finalize()
+    except Exception:  # teardown must not turn a finished session into an error
+        pass
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

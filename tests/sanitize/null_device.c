@@ -64,8 +64,24 @@ int hsd_memset_async(void *d, int v, size_t bytes)
     memset(d, v, bytes);
     return 0;
 }
+/* this thread's pending error of an asynchronous persistent Bluestein launch (null_bx_timeout
+ * = 1): kept by hsd_sync, reported once by hsd_sync_report -- the device layer's contract */
+static __thread int pl_pending;
 int hsd_sync(void) { return 0; }
+int hsd_sync_report(void)
+{
+    if (!pl_pending) return 0;
+    pl_pending = 0;
+    snprintf(err, sizeof err, "null device: persistent launch timed out");
+    return -2;
+}
 int hsd_sync_spin(void) { return 0; }
+int null_finalized;
+int hsd_finalize_device(void)
+{
+    __atomic_fetch_add(&null_finalized, 1, __ATOMIC_RELAXED);
+    return hsd_sync_report();
+}
 int hsd_select_stream(int idx)
 {
     sidx = idx;
@@ -213,18 +229,25 @@ int hsd_blue_first(const void *in, long long idist, void *out, long long odist, 
     touch_rows_w(out, odist, odist, batch, 16);
     return 0;
 }
-/* null_bx_timeout = 1: the persistent Bluestein launch reports timed-out waits (return 2, sync
- * mode); 2: the cooperative launch is refused (return 3) -- the host's three-launch path runs */
+/* null_bx_timeout = 1: the persistent Bluestein launch's waits time out -- a synchronous call
+ * gets 2 (it re-runs the rows), an asynchronous one leaves the error pending for the thread's
+ * next hsd_sync_report; 2: the grid is refused as not co-resident (3) -- the host's three-launch
+ * path runs */
 int null_bx_timeout;
 
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
-                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng)
+                 const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng, int sync)
 {
     touch_rows_r(in, idist, nsig, batch, 16);
     touch_rows_r(chirp, 0, nsig, 1, 16);
     touch_rows_r(hk, 0, 512 * 512, 1, 16);
     touch_rows_w(img, 0, (long long)(img_bytes / 16), 1, 16);
-    if (null_bx_timeout) return null_bx_timeout == 2 ? 3 : 2;
+    if (null_bx_timeout == 2) return 3;
+    if (null_bx_timeout == 1) {
+        if (sync) return 2;
+        pl_pending = 1;
+        return 0;
+    }
     touch_rows_w(out, odist, nsig, batch, 16);
     return 0;
 }

@@ -84,6 +84,12 @@ static void run_c2c(int n, int batch)
     }
 }
 
+static void *other_sync(void *rc)
+{
+    *(int *)rc = hsfft_synchronize();
+    return NULL;
+}
+
 static void run_real(int n, int batch)
 {
     fft_real_object f = fft_real_init(n, 1), iv = fft_real_init(n, -1);
@@ -220,20 +226,43 @@ int main(void)
     run_conv(1000, 1000);
     run_conv(1 << 16, 1000);
 
-    /* the persistent Bluestein launch times out (its workgroups were not all resident): the
-     * rows are re-run on the three-launch path and the fallback is counted */
+    /* the persistent Bluestein launch times out (its workgroups were not all resident):
+     * synchronous entry points (fft_exec, hsfft_exec_batched_host) re-run the rows on the
+     * three-launch path and count the fallback; the asynchronous hsfft_exec_batched leaves the
+     * error pending for ITS thread's next hsfft_synchronize(), which reports it exactly once --
+     * a later call on another plan that grows the scratch pool and builds device state does not
+     * consume it, and another thread's hsfft_synchronize() does not inherit it */
     {
         extern int null_bx_timeout;
         const long long fb0 = hsfft_bluestein_fallbacks();
         null_bx_timeout = 1;
         run_c2c(99991, 3);
         null_bx_timeout = 0;
-        /* run_c2c: 2 signs x (fft_exec, hsfft_exec_batched, hsfft_exec_batched_host) */
+        /* run_c2c: 2 signs x (fft_exec, hsfft_exec_batched_host) synchronous */
         const long long fb1 = hsfft_bluestein_fallbacks();
-        CHECK(fb1 == fb0 + 6, "bluestein fallback count %lld", fb1 - fb0);
+        CHECK(fb1 == fb0 + 4, "bluestein fallback count %lld", fb1 - fb0);
+        {
+            fft_object big = fft_init(1 << 20, 1), small = fft_init(1024, -1);
+            fft_data *x = cbuf(3LL << 20), *y = cbuf(3LL << 20);
+            CHECK(hsfft_release_scratch() == 0, "release_scratch keeps the pending error");
+            CHECK(hsfft_exec_batched(big, x, y, 3) == 0, "another plan's call succeeds: %s", hsfft_last_error());
+            fft_exec(small, x, y);
+            pthread_t ot;
+            int other_rc = 1;
+            pthread_create(&ot, NULL, other_sync, &other_rc);
+            pthread_join(ot, NULL);
+            CHECK(other_rc == 0, "another thread's hsfft_synchronize() does not inherit the error");
+            CHECK(hsfft_synchronize() == HSFFT_ERR_DEVICE, "the pending launch error is reported");
+            CHECK(hsfft_synchronize() == 0, "the launch error is reported once");
+            free(x);
+            free(y);
+            free_fft(big);
+            free_fft(small);
+        }
         run_c2c(99991, 2);
         CHECK(hsfft_bluestein_fallbacks() == fb1, "no fallback without a timeout");
-        null_bx_timeout = 2; /* the cooperative launch refused: same three-launch path */
+        CHECK(hsfft_synchronize() == 0, "no error without a timeout");
+        null_bx_timeout = 2; /* the grid refused as not co-resident: same three-launch path */
         run_c2c(99991, 3);
         null_bx_timeout = 0;
         CHECK(hsfft_bluestein_fallbacks() == fb1 + 6, "bluestein refusal count %lld", hsfft_bluestein_fallbacks() - fb1);
@@ -302,6 +331,19 @@ int main(void)
     for (int t = 0; t < 8; t++) pthread_join(th[t], NULL);
     free_fft(g_shared);
     CHECK(hsfft_release_scratch() == 0, "release_scratch 2");
+
+    /* teardown: every device's objects released (each null device finalised once), the library
+     * usable again afterwards */
+    {
+        extern int null_finalized;
+        const int f0 = null_finalized;
+        CHECK(hsfft_finalize() == 0, "finalize: %s", hsfft_last_error());
+        CHECK(null_finalized - f0 == hsfft_device_count(), "finalize visits every device: %d", null_finalized - f0);
+        run_c2c(12600, 2);
+        run_real(1 << 16, 2);
+        run_conv(300, 17);
+        CHECK(hsfft_finalize() == 0, "finalize 2");
+    }
 
     if (fails) {
         fprintf(stderr, "%d failures\n", fails);

@@ -198,16 +198,19 @@ def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
     assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
 
 
-@pytest.mark.parametrize("mode", ["refused", "sync"])
+@pytest.mark.parametrize("mode", ["refused", "refused_coop", "sync"])
 def test_bluestein_persistent_launch_contract(mode, monkeypatch):
-    """The persistent Bluestein launch is cooperative (hipLaunchCooperativeKernel).  refused: 9
-    groups = 576 workgroups of which only 512 (two per CU) can be resident, so the runtime
-    refuses the launch and the rows run on the three-launch path at once -- results bit-exact,
+    """The persistent Bluestein launch needs every workgroup resident at once.  refused: 9
+    groups = 576 workgroups of which only 512 (two per CU) can be resident, so the host's
+    occupancy check refuses the grid (refused_coop: HSFFT_BX_COOP=1, the runtime's cooperative
+    launch refuses it) and the rows run on the three-launch path at once -- results bit-exact,
     one fallback counted per call, no ~1 s wait.  sync: HSFFT_BX_SYNC=1 (the synchronous form
     with the automatic re-run) -- bit-exact, no fallback."""
     import time
     n, batch = 99991, 11
-    monkeypatch.setenv("HSFFT_BLUE_XCD", "9" if mode == "refused" else "8")
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "9" if mode.startswith("refused") else "8")
+    if mode == "refused_coop":
+        monkeypatch.setenv("HSFFT_BX_COOP", "1")
     if mode == "sync":
         monkeypatch.setenv("HSFFT_BX_SYNC", "1")
     x = T.complex_input(n, 0xC0C0, batch=batch).reshape(batch, n)
@@ -223,11 +226,78 @@ def test_bluestein_persistent_launch_contract(mode, monkeypatch):
         hsfft.synchronize()
         dt = time.perf_counter() - t0
         assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), ref), (mode, it)
-        assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0 + (1 if mode == "refused" else 0), mode
+        assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0 + (1 if mode.startswith("refused") else 0), mode
         assert dt < 0.5, f"{mode}: {dt:.3f} s for {batch} rows (a refused launch must not wait)"
     din.free()
     dout.free()
     p.close()
+
+
+def test_bluestein_async_timeout_reported_once(monkeypatch):
+    """The asynchronous error contract of the persistent launch (include/hsfft_gpu.h), with its
+    in-launch waits forced to time out (HSFFT_BX_TLIMIT=1 tick of 10 ns, HSFFT_BX_JITTER=5
+    uneven arrivals):
+      1. hsfft_exec_batched (asynchronous) returns 0 and leaves the error pending;
+      2. calls on OTHER plans that shrink / regrow the scratch pool and build device state
+         (hsfft_release_scratch, an r2c of 2^22, a drop-in fft_exec of 1024) succeed, are
+         bit-exact and do not consume the error;
+      3. the next hsfft_synchronize() returns HSFFT_ERR_DEVICE, the one after it 0 (once);
+      4. the same forced timeout in a synchronous call -- HSFFT_BX_SYNC=1, and the drop-in
+         fft_exec on host buffers -- re-runs the rows on the three-launch path: bit-exact, one
+         fallback counted per call, and nothing left pending."""
+    n, batch = 99991, 8
+    x = T.complex_input(n, 0x7173, batch=batch).reshape(batch, n)
+    ref = _oracle(x, 1, ("tlimit", n, batch))
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    L = hsfft.lib()
+    assert L.hsfft_synchronize() == 0
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "8")
+    monkeypatch.setenv("HSFFT_BX_TLIMIT", "1")
+    monkeypatch.setenv("HSFFT_BX_JITTER", "5")
+    fb0 = L.hsfft_bluestein_fallbacks()
+    assert L.hsfft_exec_batched(p.ptr, hsfft.VP(din.ptr), hsfft.VP(dout.ptr), batch) == 0
+    monkeypatch.delenv("HSFFT_BX_TLIMIT")
+    monkeypatch.delenv("HSFFT_BX_JITTER")
+    assert L.hsfft_bluestein_fallbacks() == fb0, "an asynchronous call does not re-run rows"
+    # 2. other plans' calls: scratch released and regrown, device states built
+    assert L.hsfft_release_scratch() == 0
+    nr = 1 << 22
+    xr = T.real_input(nr, 0x52, batch=1)
+    rp = hsfft.RealPlan(nr, 1)
+    dxr = hsfft.DeviceBuffer.from_array(xr)
+    dyr = hsfft.DeviceBuffer(nr * 16)
+    assert L.hsfft_r2c_batched(rp.ptr, hsfft.VP(dxr.ptr), hsfft.VP(dyr.ptr), 1) == 0
+    small = hsfft.Plan(1024, -1)
+    xs = T.complex_input(1024, 0x53)
+    ys = small.exec(xs)
+    assert T.bits_equal(ys, T.oracle_c2c(xs, -1))
+    # 3. reported exactly once, by hsfft_synchronize
+    assert L.hsfft_synchronize() == hsfft.HSFFT_ERR_DEVICE
+    assert b"timed out" in L.hsfft_last_error()
+    assert L.hsfft_synchronize() == 0
+    assert T.bits_equal(dyr.to_array(np.complex128), T.oracle_r2c(xr, 1))
+    # 4. synchronous forms re-run the rows
+    monkeypatch.setenv("HSFFT_BX_TLIMIT", "1")
+    monkeypatch.setenv("HSFFT_BX_JITTER", "5")
+    monkeypatch.setenv("HSFFT_BX_SYNC", "1")
+    dout.fill_zero()
+    fb1 = L.hsfft_bluestein_fallbacks()
+    assert L.hsfft_exec_batched(p.ptr, hsfft.VP(din.ptr), hsfft.VP(dout.ptr), batch) == 0
+    assert L.hsfft_synchronize() == 0
+    assert L.hsfft_bluestein_fallbacks() == fb1 + 1
+    assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), ref)
+    monkeypatch.delenv("HSFFT_BX_SYNC")
+    y1 = p.exec(x[3])  # the drop-in fft_exec on host buffers is synchronous by itself
+    assert L.hsfft_bluestein_fallbacks() == fb1 + 2
+    assert T.bits_equal(y1, ref[3])
+    assert L.hsfft_synchronize() == 0
+    for d in (din, dout, dxr, dyr):
+        d.free()
+    p.close()
+    rp.close()
+    small.close()
 
 
 @pytest.mark.parametrize("jitter", ["0", "2"])

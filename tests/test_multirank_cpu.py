@@ -22,11 +22,16 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_bench(nproc, batch, n):
+def run_bench(nproc, batch, n, launcher=True):
+    """launcher: under torch.distributed.run (how the driver starts N ranks); else plain
+    `bench.py --gpus N`, which starts its N rank processes itself"""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    args = [os.path.join(REPO, "bench.py"), "--gpus", str(nproc), "--dry-run", "--steps", "2", "--warmup", "1",
+            "--batch", str(batch), "--dry-n", str(n)]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(REPO, "bench.py"),
-           "--dry-run", "--steps", "2", "--warmup", "1", "--batch", str(batch), "--dry-n", str(n)]
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}"] + args if launcher else [sys.executable] + args
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
@@ -39,10 +44,10 @@ def expected_checksum(n, row0, batch):
     return float(np.abs(T.oracle_c2c(x, 1)).sum())
 
 
-@pytest.mark.parametrize("nproc", [1, 2])
-def test_bench_multirank_dry_run(nproc):
+@pytest.mark.parametrize("nproc,launcher", [(1, True), (2, True), (2, False)])
+def test_bench_multirank_dry_run(nproc, launcher):
     n, batch = 256, 3
-    out = run_bench(nproc, batch, n)
+    out = run_bench(nproc, batch, n, launcher)
     assert out["n_gpus"] == nproc and out["scaling"] == "weak" and out["per_rank_batch"] == batch
     assert out["row_starts"] == [r * batch for r in range(nproc)]  # disjoint, contiguous shards
     for r in range(nproc):
@@ -55,3 +60,12 @@ def test_row_range_partition():
     import bench
     got = [bench.row_range(r, 4096) for r in range(8)]
     assert got[0] == (0, 4096) and all(got[i][1] == got[i + 1][0] for i in range(7)) and got[7][1] == 8 * 4096
+
+
+def test_world_size_must_match_gpus():
+    """under a launcher, --gpus N with WORLD_SIZE != N is refused (a one-GPU timing must not be
+    reported as N GPUs, nor the other way round)"""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--dry-run"], cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in r.stderr
