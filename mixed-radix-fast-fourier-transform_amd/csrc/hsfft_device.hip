@@ -1248,12 +1248,20 @@ int hsd_blue_first(const void *in, long long idist, void *out, long long odist, 
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
                  long long B, int batch, int sgn, int compact)
 {
+#ifdef HSFFT_DEV_PROBES
+    /* development build: HSFFT_R2C_FUSE=2 the round-1 split kernel r8::k_r2c_last (77 vs 93
+     * GSamples/s for the fused walk) */
     const char *e = getenv("HSFFT_R2C_FUSE");
-    if (compact || !(e && atoi(e) == 2)) { /* pf::k_r2c_fused (default), 2: the older r8::k_r2c_last */
-        const int rc = pf::launch_r2c_fused(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream(), compact != 0);
-        if (rc <= 0 || compact) return rc;
+    if (!compact && e && atoi(e) == 2) return r8::launch_r2c_last(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream());
+#endif
+    /* the split walks (pf::k_r2c_walk1 / k_r2c_fused); the host calls this only for the shapes
+     * they take ([8,8,8] last pass, A == 1, B % 16 == 0) */
+    const int rc = pf::launch_r2c_fused(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream(), compact != 0);
+    if (rc == 1) {
+        snprintf(g_err, sizeof g_err, "hsd_r2c_last: no split kernel for h=%lld B=%lld", h, B);
+        return -1;
     }
-    return r8::launch_r2c_last(Z, zdist, X, xdist, tw, w2, h, B, batch, sgn, stream());
+    return rc;
 }
 
 int mr_has_variant(const hsd_pass *p)

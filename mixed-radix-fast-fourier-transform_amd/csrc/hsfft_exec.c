@@ -1068,12 +1068,14 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
         return 1; /* HSFFT_R2C_FUSE=0: pass B + k_r2c_post2 (r2c 2^22: 85 vs 93 GSamples/s fused) */
     hs_devstate *ds = devstate(e);
     if (!ds) return HSFFT_ERR_DEVICE;
-    /* HSFFT_R2C_OVL = S (measurement): the call in sub-chunks of S rows, pass A of every
+    /* HSFFT_R2C_OVL = S (measurement, development build; 27.97 / 24.75 / 23.87 vs 22.32 ms per
+     * 512 rows for S = 32 / 64 / 128): the call in sub-chunks of S rows, pass A of every
      * sub-chunk on the library stream and the split walk of sub-chunk s on the pipeline stream
      * behind pass A(s) only, so the walks (latency-bound) overlap the later pass As
      * (bandwidth-bound); Z holds every row, so nothing is reused; the library stream then waits
      * for the last walk */
-    const int ovl = env_int("HSFFT_R2C_OVL", 0);
+#ifdef HSFFT_DEV_PROBES
+    const int ovl = env_int("HSFFT_R2C_OVL", 0); /* development build only: measured slower */
     if (ovl > 0 && batch > ovl && hsd_stream_index() == 0) {
         const int ns = (batch + ovl - 1) / ovl;
         int rc = 0;
@@ -1098,6 +1100,7 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
         if (!rc) rc = hsd_event_wait(2 * (ns - 1) + 1) ? HSFFT_ERR_DEVICE : 0;
         return rc;
     }
+#endif
     int rc = launch_pass(e, ds, 0, in, idist, Z, e->M, batch, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN,
                          NULL, e->M);
     if (!rc && hsd_r2c_last(Z, e->M, X, xdist, ds->d_tw, tw2, e->M, p1->B, batch, e->sgn, compact)) {

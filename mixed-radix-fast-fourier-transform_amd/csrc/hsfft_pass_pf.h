@@ -979,56 +979,68 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
      * classes; in-process A/B per 512 rows against k_r2c_walk2 (walks of 8): 20.40 vs 20.31 ms on a
      * fast-write allocation, 20.97 vs 22.20 on a medium one, 22.25-23.60 vs 24.23-25.77 on three
      * slow ones (profiles/r04d-f_*).  HSFFT_R2C_WALK=2: walk2; 0: k_r2c_fused */
-    const int walk = env("HSFFT_R2C_WALK", 3);
+    /* product: k_r2c_walk1 (default) or, HSFFT_R2C_WALK=0, k_r2c_fused -- the independent
+     * schedule the every-word test compares against, and the compact layout's kernel.  The
+     * measured-slower walks (k_r2c_walk2, walk1's other prefetch forms, the other walk orders,
+     * the phase trace) are compiled only into the development build (-DHSFFT_DEV_PROBES) */
+    const int walk = env("HSFFT_R2C_WALK", 3) != 0 ? 3 : 0;
     if (!compact && walk != 0) {
-        const int wt_dflt = walk == 3 ? 32 : 8;
+#ifdef HSFFT_DEV_PROBES
+        const bool w2 = env("HSFFT_R2C_WALK", 3) == 2 || env("HSFFT_R2C_DEBUG", 0) != 0;
+        const int wt_dflt = w2 ? 8 : 32;
+#else
+        const int wt_dflt = 32;
+#endif
         const long long T = env("HSFFT_R2C_WT", wt_dflt) > 0 ? env("HSFFT_R2C_WT", wt_dflt) : wt_dflt,
                         W = (B / 16 + T - 1) / T;
         const long long grid = (W + 1) * (long long)batch;
         if (grid <= 0 || grid > 0x7fffffffLL) return -1;
-        /* HSFFT_R2C_NT (measurement): bit 0 non-temporal data loads, bit 1 non-temporal stores */
         typedef void (*wfn)(Args, unsigned, unsigned, unsigned);
-        const bool dbg = env("HSFFT_R2C_DEBUG", 0) != 0; /* the traced default variant */
+        /* k_r2c_walk1<SGN, PFH = true>: the next hi tile's rows loaded before the pairs phase's
+         * stores, 20.00 vs 20.15 ms per 512 rows in-process (profiles/r04i_i_c5.txt) */
+        wfn fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>;
+        int lds_bytes = R2CW1_LDS;
+        a.tile_major = 9; /* 8 rotation classes */
+        bool dbg = false;
 #ifdef HSFFT_DEV_PROBES
-        /* HSFFT_R2C_PROBE (timing only, results wrong): 1 no twiddle2 traffic, 2 no stage-2
-         * twiddle traffic, 3 neither */
-        static const wfn fws[2][8] = {
-            {k_r2c_walk2<1, 0>, k_r2c_walk2<1, 1>, k_r2c_walk2<1, 2>, k_r2c_walk2<1, 3>, k_r2c_walk2<1, 4>,
-             k_r2c_walk2<1, 5>, k_r2c_walk2<1, 6>, k_r2c_walk2<1, 7>},
-            {k_r2c_walk2<-1, 0>, k_r2c_walk2<-1, 1>, k_r2c_walk2<-1, 2>, k_r2c_walk2<-1, 3>, k_r2c_walk2<-1, 4>,
-             k_r2c_walk2<-1, 5>, k_r2c_walk2<-1, 6>, k_r2c_walk2<-1, 7>}};
-        wfn fw = fws[sgn == 1 ? 0 : 1][(dbg ? 1 : 0) | (env("HSFFT_R2C_PROBE", 0) & 3) << 1];
-#else
-        static const wfn fws[2][2] = {{k_r2c_walk2<1, 0>, k_r2c_walk2<1, 1>}, {k_r2c_walk2<-1, 0>, k_r2c_walk2<-1, 1>}};
-        wfn fw = fws[sgn == 1 ? 0 : 1][dbg ? 1 : 0];
-#endif
-        int lds_bytes = R2CW2_LDS;
-        if (walk == 3 && !dbg) { /* two walks per CU (k_r2c_walk1); the phase trace is walk2's */
-            /* bit 0 (default on since round 4): the next hi tile's rows loaded before the pairs
-             * phase's stores, 20.00 vs 20.15 ms per 512 rows in-process; bit 1: the lo rows loaded
-             * with the hi phase, 20.11 (profiles/r04i_i_c5.txt) */
-            switch (env("HSFFT_R2C_PFH", 1)) {
-            case 1: fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>; break;
-            case 2: fw = sgn == 1 ? k_r2c_walk1<1, false, true> : k_r2c_walk1<-1, false, true>; break;
-            case 3: fw = sgn == 1 ? k_r2c_walk1<1, true, true> : k_r2c_walk1<-1, true, true>; break;
-            default: fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>; break;
+        {
+            /* development build: HSFFT_R2C_WALK=2 k_r2c_walk2 (round 3's one-per-CU walk, walks of
+             * 8 by default); HSFFT_R2C_DEBUG=1 its phase trace; HSFFT_R2C_PROBE (timing only, results
+             * wrong): 1 no twiddle2 traffic, 2 no stage-2 twiddle traffic, 3 neither */
+            dbg = env("HSFFT_R2C_DEBUG", 0) != 0;
+            if (w2) {
+                static const wfn fws[2][8] = {
+                    {k_r2c_walk2<1, 0>, k_r2c_walk2<1, 1>, k_r2c_walk2<1, 2>, k_r2c_walk2<1, 3>, k_r2c_walk2<1, 4>,
+                     k_r2c_walk2<1, 5>, k_r2c_walk2<1, 6>, k_r2c_walk2<1, 7>},
+                    {k_r2c_walk2<-1, 0>, k_r2c_walk2<-1, 1>, k_r2c_walk2<-1, 2>, k_r2c_walk2<-1, 3>, k_r2c_walk2<-1, 4>,
+                     k_r2c_walk2<-1, 5>, k_r2c_walk2<-1, 6>, k_r2c_walk2<-1, 7>}};
+                fw = fws[sgn == 1 ? 0 : 1][(dbg ? 1 : 0) | (env("HSFFT_R2C_PROBE", 0) & 3) << 1];
+                lds_bytes = R2CW2_LDS;
+            } else {
+                /* walk1's other prefetch forms: HSFFT_R2C_PFH 0 none, 2 the lo rows with the hi phase,
+                 * 3 both (20.11 vs 20.00 ms, profiles/r04i_i_c5.txt) */
+                switch (env("HSFFT_R2C_PFH", 1)) {
+                case 0: fw = sgn == 1 ? k_r2c_walk1<1> : k_r2c_walk1<-1>; break;
+                case 2: fw = sgn == 1 ? k_r2c_walk1<1, false, true> : k_r2c_walk1<-1, false, true>; break;
+                case 3: fw = sgn == 1 ? k_r2c_walk1<1, true, true> : k_r2c_walk1<-1, true, true>; break;
+                default: break;
+                }
+                /* HSFFT_R2C_W1PROBE (timing only, results wrong; the default PFH walk, sgn 1): see PROBE */
+                switch (sgn == 1 ? env("HSFFT_R2C_W1PROBE", 0) : 0) {
+                case 3: fw = k_r2c_walk1<1, true, false, 3>; break;
+                case 4: fw = k_r2c_walk1<1, true, false, 4>; break;
+                case 8: fw = k_r2c_walk1<1, true, false, 8>; break;
+                case 12: fw = k_r2c_walk1<1, true, false, 12>; break;
+                case 15: fw = k_r2c_walk1<1, true, false, 15>; break;
+                case 16: fw = k_r2c_walk1<1, true, false, 16>; break;
+                case 31: fw = k_r2c_walk1<1, true, false, 31>; break;
+                default: break;
+                }
             }
-            lds_bytes = R2CW1_LDS;
-#ifdef HSFFT_DEV_PROBES
-            /* HSFFT_R2C_W1PROBE (timing only, results wrong; the default PFH walk, sgn 1): see PROBE */
-            switch (sgn == 1 ? env("HSFFT_R2C_W1PROBE", 0) : 0) {
-            case 3: fw = k_r2c_walk1<1, true, false, 3>; break;
-            case 4: fw = k_r2c_walk1<1, true, false, 4>; break;
-            case 8: fw = k_r2c_walk1<1, true, false, 8>; break;
-            case 12: fw = k_r2c_walk1<1, true, false, 12>; break;
-            case 15: fw = k_r2c_walk1<1, true, false, 15>; break;
-            case 16: fw = k_r2c_walk1<1, true, false, 16>; break;
-            case 31: fw = k_r2c_walk1<1, true, false, 31>; break;
-            default: break;
-            }
-#endif
+            /* walk orders: 0 row-major, 1 segment-major, 2 rotated, >= 3 rotation classes */
+            a.tile_major = env("HSFFT_R2C_ORDER", 9);
         }
-        a.tile_major = env("HSFFT_R2C_ORDER", 9); /* 0 row-major, 1 segment-major, 2 rotated, >= 3 classes */
+#endif
         static unsigned *s_dbg = nullptr;
         static long long s_dbg_n = 0;
         if (dbg) {

@@ -587,6 +587,7 @@ __device__ __forceinline__ void r2c_pair(double2 a, double2 c, double2 w, double
     im = (a.y - c.y + (t2 * w.x) - (t1 * w.y)) / 2.0;
 }
 
+#ifdef HSFFT_DEV_PROBES /* round 1's split kernel: development build only (HSFFT_R2C_FUSE=2) */
 __global__ __launch_bounds__(512, 4) void k_r2c_last(Args a, long long h)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -675,6 +676,7 @@ inline int launch_r2c_last(const void *Z, long long zdist, void *X, long long xd
     HCHK(hipGetLastError());
     return 0;
 }
+#endif
 
 typedef void (*kfn)(Args);
 

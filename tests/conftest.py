@@ -5,6 +5,10 @@ import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# tests/dev/: parity of the development build's measured-slower variants -- collected only when
+# asked for (HSFFT_DEV_TESTS=1, with HSFFT_LIB_PATH pointing at lib/libhsfft_dev.so)
+collect_ignore_glob = [] if os.environ.get("HSFFT_DEV_TESTS") == "1" else ["dev/*"]
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")

@@ -2,7 +2,7 @@
 
 Sampled rows against the oracle cannot see a boundary error of a walking kernel in a row that
 is not sampled (k_firstq walks column tiles, k_b512 row groups, k_row2 grid-strides rows and
-prefetches the next row's first group, k_r2c_walk2 carries one entry across tiles in eight
+prefetches the next row's first group, k_r2c_walk1 carries one entry across tiles in eight
 rotation classes).  So each config's default schedule is compared on EVERY 8-byte output word
 with an independent in-library schedule of the same transform (different kernels, different
 walk / tile structure, itself bit-exact vs the oracle in test_gpu_parity.py), on the GPU
@@ -11,8 +11,7 @@ walk / tile structure, itself bit-exact vs the oracle in test_gpu_parity.py), on
 * c2  4096 x 2^20 c2c: pf::k_firstq + pf::k_b512  vs  HSFFT_PF=0 (r8::k_pass both passes);
 * c3  65536 x 12600 c2c: mr::k_row2 (one pass)  vs  HSFFT_MR_ROW=0 (two mr::k_pass passes);
 * c5  512 x 2^22 r2c (the bench's call size): pf::k_r2c_walk1 (default since round 4)  vs
-  HSFFT_R2C_WALK=0 (pf::k_r2c_fused, one tile pair per workgroup) and vs HSFFT_R2C_WALK=2
-  (pf::k_r2c_walk2, round 3's default).
+  HSFFT_R2C_WALK=0 (pf::k_r2c_fused, one tile pair per workgroup).
 
 Reference: highSpeedFFT.c:1920-1942 (fft_exec), real.c:78-136 (fft_r2c_exec).
 Tolerance: bit-exact (0 differing words).
@@ -89,8 +88,7 @@ def test_config3_every_word(monkeypatch):
 
 def test_config5_every_word(monkeypatch):
     """512 x 2^22 reals (the bench's r2c call size): the default split walk vs one tile pair per
-    workgroup and vs the one-per-CU walk, every word of the mirrored N-bin output; sampled rows
-    vs the oracle"""
+    workgroup, every word of the mirrored N-bin output; sampled rows vs the oracle"""
     n, batch = 1 << 22, 512
     rp = hsfft.RealPlan(n, 1)
     din = hsfft.DeviceBuffer(batch * n * 8)
@@ -102,7 +100,7 @@ def test_config5_every_word(monkeypatch):
     hsfft.fill_complex(d2, batch * n, 2)
     hsfft.r2c_batched(rp, din, d1, batch)
     hsfft.synchronize()
-    for walk, name in (("0", "k_r2c_fused"), ("2", "k_r2c_walk2")):
+    for walk, name in (("0", "k_r2c_fused"),):
         monkeypatch.setenv("HSFFT_R2C_WALK", walk)
         hsfft.fill_complex(d2, batch * n, 2)
         hsfft.r2c_batched(rp, din, d2, batch)

@@ -628,11 +628,11 @@ def test_two_pass_2pow21_batched():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fuse", ["0", "1", "2"])
+@pytest.mark.parametrize("fuse", ["0", "1"])
 @pytest.mark.parametrize("n,sgn", [(1 << 19, 1), (1 << 22, 1), (1 << 22, -1), (1 << 13, 1)])
 def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
-    """the real.c split fused into the last c2c pass (HSFFT_R2C_FUSE=1, default: pf::k_r2c_walk2;
-    2: r8::k_r2c_last; 0: separate split kernel), bit-exact, both plan signs, odd batch."""
+    """the real.c split fused into the last c2c pass (HSFFT_R2C_FUSE=1, default: pf::k_r2c_walk1;
+    0: separate split kernel), bit-exact, both plan signs, odd batch."""
     monkeypatch.setenv("HSFFT_R2C_FUSE", fuse)
     x = T.real_input(n, 23, batch=3).reshape(3, n)
     rp = hsfft.RealPlan(n, sgn)
@@ -644,50 +644,22 @@ def test_r2c_fused_split(n, sgn, fuse, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wt", ["walk0", "w2:16", "w2:1", "w2:5", "w2:4096", "o1:8", "o2:8", "o2:5", "o2:32", "o2:4096",
-                                "o3:16", "o5:16", "o5:5", "o9:8"])
+@pytest.mark.parametrize("wt", ["walk0", "32", "1", "5", "4096"])
 @pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
-def test_r2c_walk(n, sgn, wt, monkeypatch):
-    """pf::k_r2c_walk2 (default split kernel of the reference-layout r2c): walks of WT tile
-    pairs per workgroup, whole-line stores with the one-entry carry between tiles.  WT=1: every
-    tile is a walk's first (partial first line, carry written at once); 5: walks of uneven
-    length and a short last walk; 4096: one walk per row (the carry reaches column B/2);
-    walk0: the one-tile-per-workgroup k_r2c_fused; o1 / o2: segment-major block order, o2 with
-    the walk start rotated per row (two carry chains per walk), o3 / o5 / o9 with 2 / 4 / 8
-    evenly spaced rotation classes.  Bit-exact vs the oracle, odd batch, stale output buffer."""
+def test_r2c_walk1(n, sgn, wt, monkeypatch):
+    """pf::k_r2c_walk1 (the default split kernel of the reference-layout r2c: two 512-thread
+    workgroups per CU, one tile buffer, stage-0/1 twiddles from global memory, 80 KiB of LDS,
+    whole-line stores with the one-entry carry between tiles, 8 rotation classes, the next hi
+    tile's rows loaded before the pairs phase's stores): walks of 32 tile pairs (default), 1
+    (every tile a walk's first: partial first line, carry written at once), 5 (uneven walks, a
+    short last walk), 4096 (one walk per row: the carry reaches column B/2); walk0: the
+    one-tile-per-workgroup pf::k_r2c_fused (HSFFT_R2C_WALK=0).  Bit-exact vs the oracle, odd
+    batch, stale output buffer.  (The measured-slower walks -- k_r2c_walk2, walk1's other
+    prefetch forms and walk orders -- are in the development build: tests/dev/.)"""
     if wt == "walk0":
         monkeypatch.setenv("HSFFT_R2C_WALK", "0")
     else:
-        monkeypatch.setenv("HSFFT_R2C_WALK", "2")
-        monkeypatch.setenv("HSFFT_R2C_WT", wt[3:])
-        monkeypatch.setenv("HSFFT_R2C_ORDER", wt[1] if wt[0] == "o" else "0")
-    x = T.real_input(n, 29, batch=3).reshape(3, n)
-    rp = hsfft.RealPlan(n, sgn)
-    din = hsfft.DeviceBuffer.from_array(x)
-    dout = hsfft.DeviceBuffer(3 * n * 16)
-    hsfft.fill_complex(dout, 3 * n, 1)  # stale data: every bin must be written
-    hsfft.r2c_batched(rp, din, dout, 3)
-    y = dout.to_array(np.complex128).reshape(3, n)
-    assert T.bits_equal(y, T.oracle_r2c(x, sgn))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("order,wt,pfh", [("9", "8", "0"), ("0", "1", "0"), ("0", "5", "0"), ("0", "4096", "0"),
-                                          ("2", "5", "0"), ("5", "16", "0"), ("1", "8", "0"), ("9", "32", "1"),
-                                          ("0", "1", "1"), ("2", "5", "1"), ("0", "4096", "1"), ("9", "32", "3"),
-                                          ("0", "1", "3"), ("2", "5", "3"), ("0", "4096", "2")])
-@pytest.mark.parametrize("n,sgn", [(1 << 22, 1), (1 << 22, -1), (1 << 19, 1), (1 << 17, -1)])
-def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
-    """pf::k_r2c_walk1 (HSFFT_R2C_WALK=3: the split walk sized for two workgroups per CU -- one
-    tile buffer, stage-0/1 twiddles from global memory, 80 KiB of LDS): walk lengths 1 (every
-    tile a walk's first), 5 (uneven walks), 4096 (one walk per row), the rotated and class
-    orders, segment-major order; pfh bit 0: the next hi tile's rows loaded before the pairs
-    phase's store burst, bit 1: the lo rows loaded with the hi phase; bit-exact vs the oracle, odd
-    batch, stale output buffer."""
-    monkeypatch.setenv("HSFFT_R2C_WALK", "3")
-    monkeypatch.setenv("HSFFT_R2C_WT", wt)
-    monkeypatch.setenv("HSFFT_R2C_ORDER", order)
-    monkeypatch.setenv("HSFFT_R2C_PFH", pfh)
+        monkeypatch.setenv("HSFFT_R2C_WT", wt)
     x = T.real_input(n, 31, batch=3).reshape(3, n)
     rp = hsfft.RealPlan(n, sgn)
     din = hsfft.DeviceBuffer.from_array(x)
@@ -696,28 +668,6 @@ def test_r2c_walk1(n, sgn, order, wt, pfh, monkeypatch):
     hsfft.r2c_batched(rp, din, dout, 3)
     y = dout.to_array(np.complex128).reshape(3, n)
     assert T.bits_equal(y, T.oracle_r2c(x, sgn))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("n,batch,ovl", [(1 << 22, 5, 2), (1 << 17, 7, 3), (1 << 17, 4, 1)])
-def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
-    """HSFFT_R2C_OVL: pass A of each sub-chunk on the library stream, the split walk on the
-    pipeline stream behind it (uneven last sub-chunk, one-row sub-chunks); bit-exact vs the
-    oracle, and the library stream is ordered after the last walk (a second call into the
-    same buffers right after must see the first call's rows complete)"""
-    monkeypatch.setenv("HSFFT_R2C_OVL", str(ovl))
-    x = T.real_input(n, 35, batch=batch).reshape(batch, n)
-    rp = hsfft.RealPlan(n, 1)
-    din = hsfft.DeviceBuffer.from_array(x)
-    dout = hsfft.DeviceBuffer(batch * n * 16)
-    hsfft.fill_complex(dout, batch * n, 1)
-    hsfft.r2c_batched(rp, din, dout, batch)
-    y1 = dout.to_array(np.complex128).reshape(batch, n)
-    hsfft.r2c_batched(rp, din, dout, batch)
-    y2 = dout.to_array(np.complex128).reshape(batch, n)
-    ref = T.oracle_r2c(x, 1)
-    assert T.bits_equal(y1, ref)
-    assert T.bits_equal(y2, ref)
 
 
 @pytest.mark.gpu
@@ -764,7 +714,6 @@ def test_12600_row_kernel_edited_twiddles_refresh(monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"HSFFT_ROW_F23": "0"}, {"HSFFT_MR_ROW": "0"}, {"HSFFT_ROW_F45": "0"},
-                                 {"HSFFT_ROW_TWN": "3"},
                                  {"HSFFT_ROW_TWN": "0"}])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64])
@@ -776,9 +725,8 @@ def test_12600_row_kernel_variants(env, sgn, rows, monkeypatch):
     mr::k_row2 (default: 512 threads, stages 0-1 and 2-3 fused in registers, stages 4-5 fused
     over thread pairs (F45) with the stage-5 twiddles from the plan's transposed copy of that
     stage's block, the next row's first input group prefetched into registers), the same with
-    stages 4 and 5 apart, without the stage 2-3 fusion, with F45's stage-5 twiddles of steps
-    1-3 copied into LDS per row (HSFFT_ROW_TWN=3) or read from the table as laid out (=0), and
-    the two mixed-radix passes."""
+    stages 4 and 5 apart, without the stage 2-3 fusion, with F45's stage-5 twiddles read from
+    the table as laid out (HSFFT_ROW_TWN=0), and the two mixed-radix passes."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 12600
