@@ -575,6 +575,7 @@ static size_t g_pin_sz[HS_MAX_DEV];
  * other library calls concurrently. */
 int hsfft_finalize(void)
 {
+    g_errbuf[0] = 0;
     int rc = hs_require_gpu();
     if (rc) return rc;
     const int cur = hsd_get_device();
@@ -587,7 +588,10 @@ int hsfft_finalize(void)
             continue;
         }
         const int dl = hs_lock_device();
-        if (hsd_sync() && !rc) rc = HSFFT_ERR_DEVICE;
+        if (hsd_sync() && !rc) {
+            hs_seterr("hsfft_finalize: %s", hsd_errstr());
+            rc = HSFFT_ERR_DEVICE;
+        }
         for (int c = 0; c < HS_NSCRATCH; c++) {
             hsd_free(g_scr[d][c]);
             g_scr[d][c] = NULL;
@@ -1318,7 +1322,15 @@ int hsfft_free(void *p) { return hsd_free(p) ? HSFFT_ERR_DEVICE : 0; }
 int hsfft_memcpy_h2d(void *d, const void *h, size_t n) { return hsd_h2d(d, h, n) ? HSFFT_ERR_DEVICE : 0; }
 int hsfft_memcpy_d2h(void *h, const void *d, size_t n) { return hsd_d2h(h, d, n) ? HSFFT_ERR_DEVICE : 0; }
 int hsfft_memset(void *d, int v, size_t n) { return hsd_memset_async(d, v, n) ? HSFFT_ERR_DEVICE : 0; }
-int hsfft_synchronize(void) { return hsd_sync_report() ? HSFFT_ERR_DEVICE : 0; }
+int hsfft_synchronize(void)
+{
+    g_errbuf[0] = 0;
+    if (hsd_sync_report()) {
+        hs_seterr("hsfft_synchronize: %s", hsd_errstr());
+        return HSFFT_ERR_DEVICE;
+    }
+    return 0;
+}
 void *hsfft_get_stream(void) { return hsd_stream(); }
 
 int hsfft_plan_refresh(fft_object obj)

@@ -576,12 +576,17 @@ __device__ __forceinline__ double lane_swap(double v)
 }
 
 /* exchange fused_ab's outputs (as xchg1_ab_std writes them) into F45's stage-4 inputs: thread
- * (g, h) reads butterflies ml = 4h + c (c < 4) at kloc = g, point i at (ml + 8i)*G45 + g */
-template <int RA, int RB, int L, int P, int TPG>
+ * (g, h) reads butterflies ml = 4h + c (c < 4) at kloc = g, point i at (ml + 8i)*PITCH + g.
+ * The image is [56][PITCH] doubles.  PITCH = G45 (225) is the packed layout; a padded pitch
+ * with PITCH % 8 == 4 (260) puts the rows of thread A (h = 0) and thread B (h = 1) of one
+ * 32-lane ds_read_b64 group 32 banks apart (4 rows = 8*PITCH dwords = 32 mod 64), and steps c
+ * 2080 B apart, beyond ds_read2_b64's offset range: every read a conflict-free ds_read_b64 */
+template <int RA, int RB, int L, int P, int TPG, int PITCH = P / 56>
 __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 {
     constexpr int Q = RA * RB, NG2 = P / Q, NGT = cdiv(NG2, TPG), LN = L * Q, G45 = P / 56;
     static_assert(LN == G45, "F45 follows F23 at L = P / 56");
+    static_assert(PITCH >= G45, "F45 image pitch");
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < NGT; c++) {
@@ -591,7 +596,7 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 #pragma unroll
         for (int jj = 0; jj < RA; jj++)
 #pragma unroll
-            for (int jq = 0; jq < RB; jq++) ld[mlp * LN + kloc + jj * L + jq * L * RA] = x[c * Q + jj * RB + jq];
+            for (int jq = 0; jq < RB; jq++) ld[mlp * PITCH + kloc + jj * L + jq * L * RA] = x[c * Q + jj * RB + jq];
     }
     __syncthreads();
     const int h = jt & 1;
@@ -600,7 +605,7 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 #pragma unroll
     for (int c = 0; c < 4; c++)
 #pragma unroll
-        for (int i = 0; i < 7; i++) x[c * 7 + i] = ld[(4 * h + c + 8 * i) * G45 + g];
+        for (int i = 0; i < 7; i++) x[c * 7 + i] = ld[(4 * h + c + 8 * i) * PITCH + g];
 }
 
 /* TWN 3: the stage-5 twiddles of steps d >= 1 (k-blocks jj = 1, 2, 3 of thread A and 5, 6 of
@@ -785,8 +790,9 @@ constexpr int ROW_PRE_PTS = 8448;
 /* PF: the inputs of the next row's first PF 9-point groups (37 % of a row per group at
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
+/* XP (F45): the pitch of the F45 exchange image in doubles (0: packed, P/56) -- xchg1_ab_g45 */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false, bool F45 = false, int TWN = 0>
+          bool F23 = false, bool F45 = false, int TWN = 0, int XP = 0>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
@@ -802,7 +808,8 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     static_assert(!PRE || (F01 && NT % 2 == 0 && 2 * NT * 8 + ROW_PRE_PTS * 16 <= 160 * 1024 &&
                            ROW_PRE_PTS >= 2 * (P / R0) && P * 8 <= ROW_PRE_PTS * 16),
                   "row prefetch layout");
-    double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + P + (P & 1));
+    constexpr int PG45 = XP > 0 ? XP : P / 56, IMGD = F45 && 56 * PG45 > P ? 56 * PG45 : P; /* image doubles */
+    double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + IMGD + (IMGD & 1));
     double *img = PRE ? ldsd + 2 * NT : ldsd;
     const int jt0 = threadIdx.x, sgn = a.sgn;
     /* LDS copy of the stage-1..4 twiddles, transposed within each stage's block [L-1, RL-1):
@@ -881,8 +888,8 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         if constexpr (F45) { /* stages 2-3 fused, then 4-5 fused over thread pairs: two exchanges */
             fused_ab<R2, R3, LS::Lloc(2), P, TPG, CONJ>(xr, xi, ltw, jt, sgn);
             mark(a, tp, 2);
-            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
-            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
+            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG, PG45>(xr, img, jt);
+            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG, PG45>(xi, img, jt);
             mark(a, tp, 3);
             if constexpr (TWN == 3) {
                 __syncthreads(); /* every wave has read the image */
@@ -1073,6 +1080,12 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * it: 6.11 vs 5.98 ms (round 4, removed) */
         size_t lds = lds0;
 #ifdef HSFFT_DEV_PROBES
+        /* round 5 A/B: HSFFT_ROW_XP=260 -- the F45 exchange image with a padded pitch */
+        if (f45 && twn4 && getenv("HSFFT_ROW_XP") && atoi(getenv("HSFFT_ROW_XP")) == 260) {
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4, 260>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4, 260>;
+            lds = (size_t)56 * 260 * sizeof(double) + (size_t)NT * sizeof(double2);
+        }
         /* development build only (measurement): HSFFT_ROW_TWN=2 constant stage-5 twiddles, results
          * wrong (5.46-5.49 ms: what the twiddle loads cost); 3 those of steps 1-3 copied into LDS
          * before the row's stores (6.20 vs 5.89 ms).  Loading step d+1's run before step d's
