@@ -1003,8 +1003,8 @@ int hsd_select_stream(int idx)
     return 0;
 }
 
-/* The CU-masked stream pair of the current device: stream 4 runs on `num` of every `den` CU-mask
- * bits (spread evenly over the bits), stream 5 on the others.  Rebuilt when the split changes;
+/* The CU-masked stream pair of the current device: stream 4 runs on `num` of every `den` CUs of
+ * each XCD, stream 5 on the others.  Rebuilt when the split changes;
  * 0 on success. */
 int hsd_masked_streams(int num, int den)
 {
@@ -1026,8 +1026,11 @@ int hsd_masked_streams(int num, int den)
     memset(m, 0, sizeof m);
     const int words = (ncu + 31) / 32;
     if (words > 16) return -1;
+    /* mask bit i selects CU i / 8 of XCD i % 8 (measured: tools/experiments/cu_mask.hip); a mask
+     * that leaves an XCD without CUs is ignored by the runtime (the stream then runs on every
+     * CU), so both masks keep the same CUs of every XCD: stream 4 the CUs c with c % den < num */
     for (int i = 0; i < ncu; i++) {
-        const bool a = ((i + 1) * num) / den != (i * num) / den;
+        const bool a = (i / 8) % den < num;
         m[a ? 0 : 1][i / 32] |= 1u << (i % 32);
     }
     for (int k = 0; k < 2; k++) HCHK(hipExtStreamCreateWithCUMask(&g_mstream[dev][k], (uint32_t)words, m[k]));

@@ -83,6 +83,17 @@ static std::vector<uint32_t> mask_frac(int ncu_total, int num, int den, bool com
     return m;
 }
 
+// balanced over the XCDs if bit i is CU i / 8 of XCD i % 8: keep CUs c (= i / 8) with c % den < num
+static std::vector<uint32_t> mask_xcd(int ncu_total, int num, int den, bool complement)
+{
+    std::vector<uint32_t> m((ncu_total + 31) / 32, 0);
+    for (int i = 0; i < ncu_total; i++) {
+        const bool on = (i / 8) % den < num;
+        if (on != complement) m[i / 32] |= 1u << (i % 32);
+    }
+    return m;
+}
+
 static int popc(const std::vector<uint32_t> &m)
 {
     int c = 0;
@@ -149,6 +160,10 @@ int main()
     layout("every 2nd bit", mask_every(ncu, 2, 0), d_out, grid);
     layout("3 of every 4 bits", mask_frac(ncu, 3, 4, false), d_out, grid);
     layout("1 of every 4 bits", mask_frac(ncu, 3, 4, true), d_out, grid);
+    layout("xcd-balanced 1/4 (c%4==0)", mask_xcd(ncu, 1, 4, false), d_out, grid);
+    layout("xcd-balanced 3/4 (c%4!=0)", mask_xcd(ncu, 1, 4, true), d_out, grid);
+    layout("xcd-balanced 1/2 (c%2==0)", mask_xcd(ncu, 1, 2, false), d_out, grid);
+    layout("xcd-balanced 1/8 (c%8==0)", mask_xcd(ncu, 1, 8, false), d_out, grid);
 
     const long long n = (8LL << 30) / 16; // 8 GiB per buffer
     double2 *a, *b, *c, *d;
@@ -160,17 +175,17 @@ int main()
     CK(hipMemset(c, 0, n * 16));
     const int fr[][2] = {{1, 8}, {1, 4}, {1, 2}, {3, 4}, {1, 1}};
     for (auto &f : fr) {
-        std::vector<uint32_t> m = mask_frac(ncu, f[0], f[1], false);
+        std::vector<uint32_t> m = mask_xcd(ncu, f[0], f[1], false);
         hipStream_t s;
         CK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()));
         const float ms = copy_ms(s, a, b, n, 3);
-        printf("copy 8 GiB on %3d CUs (%d/%d of the bits): %.3f ms = %.0f GB/s\n", popc(m), f[0], f[1], ms,
+        printf("copy 8 GiB on %3d CUs (%d/%d of each XCD's CUs): %.3f ms = %.0f GB/s\n", popc(m), f[0], f[1], ms,
                2.0 * n * 16 / (ms * 1e-3) / 1e9);
         CK(hipStreamDestroy(s));
     }
     // two copies at once on complementary masks (3/4 + 1/4)
     {
-        std::vector<uint32_t> m1 = mask_frac(ncu, 3, 4, false), m2 = mask_frac(ncu, 3, 4, true);
+        std::vector<uint32_t> m1 = mask_xcd(ncu, 1, 4, true), m2 = mask_xcd(ncu, 1, 4, false);
         hipStream_t s1, s2;
         CK(hipExtStreamCreateWithCUMask(&s1, (uint32_t)m1.size(), m1.data()));
         CK(hipExtStreamCreateWithCUMask(&s2, (uint32_t)m2.size(), m2.data()));
