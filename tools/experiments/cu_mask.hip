@@ -103,6 +103,7 @@ static int popc(const std::vector<uint32_t> &m)
 
 static void layout(const char *name, const std::vector<uint32_t> &m, unsigned *d_out, int grid)
 {
+    printf("layout %-28s: launching\n", name);
     hipStream_t s;
     CK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()));
     CK(hipMemsetAsync(d_out, 0xff, (size_t)grid * 8, s));
@@ -145,14 +146,20 @@ static float copy_ms(hipStream_t s, const double2 *a, double2 *b, long long n, i
     return ms / iters;
 }
 
-int main()
+int main(int argc, char **argv)
 {
+    setvbuf(stdout, NULL, _IOLBF, 0); /* a stall must still show how far the run got */
+    const char *only = argc > 1 ? argv[1] : "all"; /* layout | copy | concurrent | all */
     int ncu = 0;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     printf("CUs %d\n", ncu);
     const int grid = 8192;
     unsigned *d_out;
     CK(hipMalloc(&d_out, (size_t)grid * 8));
+    const bool do_layout = !strcmp(only, "all") || !strcmp(only, "layout");
+    const bool do_copy = !strcmp(only, "all") || !strcmp(only, "copy");
+    const bool do_conc = !strcmp(only, "all") || !strcmp(only, "concurrent");
+    if (do_layout) {
     layout("all", mask_first(ncu, ncu), d_out, grid);
     layout("first 32 bits", mask_first(ncu, 32), d_out, grid);
     layout("first 128 bits", mask_first(ncu, 128), d_out, grid);
@@ -164,6 +171,7 @@ int main()
     layout("xcd-balanced 3/4 (c%4!=0)", mask_xcd(ncu, 1, 4, true), d_out, grid);
     layout("xcd-balanced 1/2 (c%2==0)", mask_xcd(ncu, 1, 2, false), d_out, grid);
     layout("xcd-balanced 1/8 (c%8==0)", mask_xcd(ncu, 1, 8, false), d_out, grid);
+    }
 
     const long long n = (8LL << 30) / 16; // 8 GiB per buffer
     double2 *a, *b, *c, *d;
@@ -175,8 +183,10 @@ int main()
     CK(hipMemset(c, 0, n * 16));
     const int fr[][2] = {{1, 8}, {1, 4}, {1, 2}, {3, 4}, {1, 1}};
     for (auto &f : fr) {
+        if (!do_copy) break;
         std::vector<uint32_t> m = mask_xcd(ncu, f[0], f[1], false);
         hipStream_t s;
+        printf("copy on %d/%d of each XCD's CUs: launching\n", f[0], f[1]);
         CK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()));
         const float ms = copy_ms(s, a, b, n, 3);
         printf("copy 8 GiB on %3d CUs (%d/%d of each XCD's CUs): %.3f ms = %.0f GB/s\n", popc(m), f[0], f[1], ms,
@@ -184,7 +194,7 @@ int main()
         CK(hipStreamDestroy(s));
     }
     // two copies at once on complementary masks (3/4 + 1/4)
-    {
+    if (do_conc) {
         std::vector<uint32_t> m1 = mask_xcd(ncu, 1, 4, true), m2 = mask_xcd(ncu, 1, 4, false);
         hipStream_t s1, s2;
         CK(hipExtStreamCreateWithCUMask(&s1, (uint32_t)m1.size(), m1.data()));
