@@ -63,8 +63,7 @@ int set_err(hipError_t e, const char *what)
 
 hipStream_t g_stream2[HS_MAX_DEV], g_stream3[HS_MAX_DEV];
 std::atomic<bool> g_stream2_init[HS_MAX_DEV], g_stream3_init[HS_MAX_DEV];
-thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream, 3: this thread's own,
-                                * 4 / 5: the CU-masked pair (hsd_masked_streams) */
+thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream, 3: this thread's own */
 thread_local hipStream_t t_own[HS_MAX_DEV]; /* per-thread streams (concurrent small fft_exec calls) */
 
 int cur_dev()
@@ -78,16 +77,10 @@ hipStream_t primary() { return lazy_stream(g_stream, g_stream_init, cur_dev()); 
 
 /* the stream kernels are launched on: the library stream, or (inside a pipelined chain)
  * the second stream that runs pass B of chunk c while pass A of chunk c+1 runs */
-/* two streams whose kernels run on complementary CU sets (hipExtStreamCreateWithCUMask), per
- * device; (re)built by hsd_masked_streams under g_init_mtx */
-hipStream_t g_mstream[HS_MAX_DEV][2];
-int g_mstream_split[HS_MAX_DEV];
-
 hipStream_t stream()
 {
     if (t_sidx == 0) return primary();
     const int dev = cur_dev();
-    if (t_sidx >= 4) return g_mstream[dev][t_sidx - 4] ? g_mstream[dev][t_sidx - 4] : primary();
     if (t_sidx == 3) {
         if (!t_own[dev] && hipStreamCreateWithFlags(&t_own[dev], hipStreamNonBlocking) != hipSuccess) t_own[dev] = 0;
         return t_own[dev];
@@ -980,13 +973,6 @@ int hsd_finalize_device(void)
         for (int k = 0; k < 2 * HS_MAX_PASSES; k++) (void)hipEventDestroy(g_pev[dev][k]);
         g_timer_init[dev].store(false, std::memory_order_release);
     }
-    for (int k = 0; k < 2; k++)
-        if (g_mstream[dev][k]) {
-            (void)hipStreamSynchronize(g_mstream[dev][k]);
-            (void)hipStreamDestroy(g_mstream[dev][k]);
-            g_mstream[dev][k] = 0;
-        }
-    g_mstream_split[dev] = 0;
     for (int s = 0; s < 3; s++)
         if (flags[s][dev].load(std::memory_order_acquire)) {
             if (tabs[s][dev]) (void)hipStreamDestroy(tabs[s][dev]);
@@ -999,42 +985,7 @@ int hsd_finalize_device(void)
 
 int hsd_select_stream(int idx)
 {
-    t_sidx = idx < 0 || idx > 5 ? 0 : idx;
-    return 0;
-}
-
-/* The CU-masked stream pair of the current device: stream 4 runs on `num` of every `den` CUs of
- * each XCD, stream 5 on the others.  Rebuilt when the split changes;
- * 0 on success. */
-int hsd_masked_streams(int num, int den)
-{
-    const int dev = cur_dev();
-    if (num < 1 || den <= num) return -1;
-    std::lock_guard<std::mutex> g(g_init_mtx);
-    const int key = num * 1024 + den;
-    if (g_mstream_split[dev] == key && g_mstream[dev][0] && g_mstream[dev][1]) return 0;
-    for (int k = 0; k < 2; k++)
-        if (g_mstream[dev][k]) {
-            (void)hipStreamSynchronize(g_mstream[dev][k]);
-            (void)hipStreamDestroy(g_mstream[dev][k]);
-            g_mstream[dev][k] = 0;
-        }
-    g_mstream_split[dev] = 0;
-    int ncu = 0;
-    HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    uint32_t m[2][16];
-    memset(m, 0, sizeof m);
-    const int words = (ncu + 31) / 32;
-    if (words > 16) return -1;
-    /* mask bit i selects CU i / 8 of XCD i % 8 (measured: tools/experiments/cu_mask.hip); a mask
-     * that leaves an XCD without CUs is ignored by the runtime (the stream then runs on every
-     * CU), so both masks keep the same CUs of every XCD: stream 4 the CUs c with c % den < num */
-    for (int i = 0; i < ncu; i++) {
-        const bool a = (i / 8) % den < num;
-        m[a ? 0 : 1][i / 32] |= 1u << (i % 32);
-    }
-    for (int k = 0; k < 2; k++) HCHK(hipExtStreamCreateWithCUMask(&g_mstream[dev][k], (uint32_t)words, m[k]));
-    g_mstream_split[dev] = key;
+    t_sidx = idx < 0 || idx > 3 ? 0 : idx;
     return 0;
 }
 

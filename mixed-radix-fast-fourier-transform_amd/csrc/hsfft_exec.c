@@ -1079,48 +1079,6 @@ int hs_r2c_fused(hs_entry *e, const void *in, long long idist, void *Z, void *X,
      * (bandwidth-bound); Z holds every row, so nothing is reused; the library stream then waits
      * for the last walk */
 #ifdef HSFFT_DEV_PROBES
-    /* HSFFT_R2C_CUSPLIT = den (measurement, development build): the call in sub-chunks of
-     * HSFFT_R2C_SUB rows (default 64), pass A of every sub-chunk on a stream masked to 1 of every
-     * den CUs and the split walk on a stream masked to the others, the walk of sub-chunk s behind
-     * pass A(s) only -- so the latency-bound walk (~3.8 TB/s) and the bandwidth-bound pass A run
-     * at once on disjoint CUs.  Every sub-chunk has its own rows of Z (no reuse inside the
-     * call); both streams first wait for the library stream, which then waits for the last walk */
-    const int cus = env_int("HSFFT_R2C_CUSPLIT", 0), sub = env_int("HSFFT_R2C_SUB", 64);
-    if (cus > 1 && sub > 0 && batch > sub && hsd_stream_index() == 0 && (batch + sub - 1) / sub <= 60) {
-        if (hsd_masked_streams(1, cus)) {
-            hs_seterr("CU-masked streams: %s", hsd_errstr());
-            return HSFFT_ERR_DEVICE;
-        }
-        const int ns = (batch + sub - 1) / sub;
-        int rc = hsd_event_record(0) ? HSFFT_ERR_DEVICE : 0;
-        hsd_select_stream(4);
-        if (!rc) rc = hsd_event_wait(0) ? HSFFT_ERR_DEVICE : 0;
-        hsd_select_stream(5);
-        if (!rc) rc = hsd_event_wait(0) ? HSFFT_ERR_DEVICE : 0;
-        for (int s = 0; s < ns && !rc; s++) {
-            const long long r0 = (long long)s * sub;
-            const int nb = (int)(batch - r0 < sub ? batch - r0 : sub);
-            void *Zs = (char *)Z + r0 * e->M * (long long)sizeof(fft_data);
-            hsd_select_stream(4);
-            rc = launch_pass(e, ds, 0, (const char *)in + r0 * idist * (long long)sizeof(fft_data), idist, Zs, e->M,
-                             nb, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL, HS_STORE_PLAIN, NULL, e->M);
-            if (!rc) rc = hsd_event_record(2 + s) ? HSFFT_ERR_DEVICE : 0;
-            hsd_select_stream(5);
-            if (!rc) rc = hsd_event_wait(2 + s) ? HSFFT_ERR_DEVICE : 0;
-            if (!rc && hsd_r2c_last(Zs, e->M, (char *)X + r0 * xdist * (long long)sizeof(fft_data), xdist, ds->d_tw,
-                                    tw2, e->M, p1->B, nb, e->sgn, compact)) {
-                hs_seterr("r2c last pass: %s", hsd_errstr());
-                rc = HSFFT_ERR_DEVICE;
-            }
-        }
-        hsd_select_stream(5);
-        if (!rc) rc = hsd_event_record(1) ? HSFFT_ERR_DEVICE : 0;
-        hsd_select_stream(4);
-        if (!rc) rc = hsd_event_record(62) ? HSFFT_ERR_DEVICE : 0;
-        hsd_select_stream(0);
-        if (!rc) rc = hsd_event_wait(1) || hsd_event_wait(62) ? HSFFT_ERR_DEVICE : 0;
-        return rc;
-    }
     const int ovl = env_int("HSFFT_R2C_OVL", 0); /* development build only: measured slower */
     if (ovl > 0 && batch > ovl && hsd_stream_index() == 0) {
         const int ns = (batch + ovl - 1) / ovl;

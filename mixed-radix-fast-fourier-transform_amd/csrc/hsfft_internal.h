@@ -88,10 +88,7 @@ int hsd_sync_spin(void);          /* hsd_sync polling an event instead of a bloc
 /* release every device object of the device layer on the current device (streams, events,
  * persistent-launch counters, this thread's error words); re-created on demand */
 int hsd_finalize_device(void);
-int hsd_select_stream(int idx);   /* 0 library stream, 1 pipeline / H2D, 2 D2H, 3 this thread's own stream,
-                                   * 4 / 5 the CU-masked pair */
-/* (re)build the current device's CU-masked stream pair: 4 on num of every den mask bits, 5 on the rest */
-int hsd_masked_streams(int num, int den);
+int hsd_select_stream(int idx);   /* 0 library stream, 1 pipeline / H2D, 2 D2H, 3 this thread's own stream */
 int hsd_stream_index(void);       /* the calling thread's selected stream */
 int hsd_h2d_async(void *d, const void *h, size_t bytes);   /* on the selected stream */
 int hsd_d2h_async(void *h, const void *d, size_t bytes);

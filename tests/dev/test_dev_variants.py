@@ -109,25 +109,3 @@ def test_12600_row_stage5_twiddles_through_lds(sgn, rows, monkeypatch):
     hsfft.exec_batched(p, din, dout, rows)
     y = dout.to_array(np.complex128).reshape(rows, n)
     assert T.bits_equal(y, T.oracle_c2c(x, sgn))
-
-
-@pytest.mark.parametrize("split,sub,batch", [("4", "2", 7), ("3", "1", 3), ("4", "64", 130)])
-def test_r2c_cu_split_pipeline(split, sub, batch, monkeypatch):
-    """HSFFT_R2C_CUSPLIT: pass A of each sub-chunk on a CU-masked stream, the split walk on the
-    complementary CUs behind it; odd sub-chunks, a ragged last one; a second call into the same
-    buffers must see the first call's rows complete"""
-    monkeypatch.setenv("HSFFT_R2C_CUSPLIT", split)
-    monkeypatch.setenv("HSFFT_R2C_SUB", sub)
-    n = 1 << 17 if batch > 8 else 1 << 22
-    x = T.real_input(n, 37, batch=batch).reshape(batch, n)
-    rp = hsfft.RealPlan(n, 1)
-    din = hsfft.DeviceBuffer.from_array(x)
-    dout = hsfft.DeviceBuffer(batch * n * 16)
-    hsfft.fill_complex(dout, batch * n, 1)
-    hsfft.r2c_batched(rp, din, dout, batch)
-    y1 = dout.to_array(np.complex128).reshape(batch, n)
-    hsfft.r2c_batched(rp, din, dout, batch)
-    y2 = dout.to_array(np.complex128).reshape(batch, n)
-    ref = T.oracle_r2c(x, 1)
-    assert T.bits_equal(y1, ref)
-    assert T.bits_equal(y2, ref)

@@ -88,7 +88,6 @@ int hsd_select_stream(int idx)
     return 0;
 }
 int hsd_stream_index(void) { return sidx; }
-int hsd_masked_streams(int num, int den) { return num >= 1 && den > num ? 0 : -1; }
 int hsd_h2d_async(void *d, const void *h, size_t bytes) { return hsd_h2d(d, h, bytes); }
 int hsd_d2h_async(void *h, const void *d, size_t bytes) { return hsd_d2h(h, d, bytes); }
 int hsd_stream_sync(void) { return 0; }
