@@ -640,6 +640,31 @@ __device__ __forceinline__ void f45_tw_copy(const double2 *tw, double2 *img, dou
     }
 }
 
+/* TWN 5: the stage-5 twiddles of steps 1 and 2 (k-blocks jj = 1, 2 of thread A and 5, 6 of thread
+ * B: 4 blocks x 7 x 225 entries = 100800 B, exactly the exchange image) copied by LDS-DMA from the
+ * plan's transposed copy (tw + P, [i-1][k]) into the free exchange image right after the last
+ * exchange's reads -- before any store of the row -- as [slot][i-1][g]; steps 1 and 2 then read
+ * them from LDS, so their twiddle waits no longer wait for the earlier steps' stores (vmcnt counts
+ * loads and stores in one order).  Steps 0 and 3 read the transposed copy from global (TWN 4). */
+constexpr int F45_DMA_SLOTS = 4;
+__device__ __forceinline__ void glds16(const double2 *g, double2 *lds_base);
+template <int P, int TPG>
+__device__ __forceinline__ void f45_tw_dma(const double2 *twt, double2 *img, int jt)
+{
+    constexpr int G45 = P / 56, L5 = 7 * G45, NE = F45_DMA_SLOTS * 7 * G45, NW = TPG / 64;
+    static_assert(NE * 16 <= P * 8, "the DMA'd twiddles fit the exchange image");
+    const int lane = jt & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(jt >> 6);
+#pragma unroll 1
+    for (int e0 = wave * 64; e0 < NE; e0 += NW * 64) { /* e0 wave-uniform: the LDS-DMA base */
+        const int e = e0 + lane, ec = e < NE ? e : NE - 1;
+        const int slot = ec / (7 * G45), r = ec % (7 * G45), i = r / G45, g = r % G45;
+        const int jj = slot < 2 ? slot + 1 : slot + 3; /* slots 0, 1: A's jj = 1, 2; 2, 3: B's jj = 5, 6 */
+        if (e < NE) glds16(twt + i * L5 + jj * G45 + g, img + e0);
+    }
+    asm volatile("" ::: "memory"); /* later loads / stores stay behind the DMA */
+}
+
 /* stages 4 (radix 7) and 5 (radix 8) of the pair's group, then the row's stores */
 template <int P, int TPG, bool CONJ, int TWN = 0>
 __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const double2 *ltw, const double2 *tw,
@@ -671,6 +696,12 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
     const double2 *twb = tw + (L5 - 1);
 #pragma unroll
     for (int d = 0; d < 4; d++) {
+        if constexpr (TWN == 5) {
+            if (d == 1) { /* this wave's DMA (older than step 0's loads and 8 stores) has landed, */
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); /* then every wave's */
+                __syncthreads();
+            }
+        }
         const int jj = h ? 4 + d : d, da = d < 3 ? 4 + d : 6;
         double zr[8], zi[8];
 #pragma unroll
@@ -695,6 +726,9 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
             } else if constexpr (TWN == 4) {
                 /* the plan's transposed copy of this stage's block at tw + P ([i-1][k]) */
                 t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
+            } else if constexpr (TWN == 5) {
+                if (d == 1 || d == 2) t = timg[((h ? d + 1 : d - 1) * 7 + i - 1) * G45 + g];
+                else t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
             } else t = pf::ldg(twb, (7 * k + i - 1) * 16u);
             hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
         }
@@ -896,6 +930,10 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
                 f45_tw_copy<P, TPG>(a.tw, reinterpret_cast<double2 *>(img), ltw + NT, jt);
                 __syncthreads();
             }
+            if constexpr (TWN == 5) {
+                __syncthreads(); /* every wave has read the image */
+                f45_tw_dma<P, TPG>(a.tw + P, reinterpret_cast<double2 *>(img), jt);
+            }
             fused45_pair<P, TPG, CONJ, TWN>(xr, xi, ltw, a.tw, out, jt, sgn, reinterpret_cast<const double2 *>(img),
                                             ltw + NT);
             mark(a, tp, 6);
@@ -1080,7 +1118,12 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * it: 6.11 vs 5.98 ms (round 4, removed) */
         size_t lds = lds0;
 #ifdef HSFFT_DEV_PROBES
-        /* round 5 A/B: HSFFT_ROW_XP=260 -- the F45 exchange image with a padded pitch */
+        /* round 5 A/B: HSFFT_ROW_TWN=5 -- steps 1-2 of the stage-5 twiddles by LDS-DMA into the image */
+        if (f45 && twn4 && etwn && atoi(etwn) == 5)
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 5>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 5>;
+        /* round 5 A/B: HSFFT_ROW_XP=260 -- the F45 exchange image with a padded pitch (5.741 vs
+         * 5.749 ms per 65536 rows: not kept, profiles/r05b_c3_xp_ab_and_cu_mask.txt) */
         if (f45 && twn4 && getenv("HSFFT_ROW_XP") && atoi(getenv("HSFFT_ROW_XP")) == 260) {
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4, 260>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4, 260>;
