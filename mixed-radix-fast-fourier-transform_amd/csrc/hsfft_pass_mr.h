@@ -646,20 +646,20 @@ __device__ __forceinline__ void f45_tw_copy(const double2 *tw, double2 *img, dou
  * exchange's reads -- before any store of the row -- as [slot][i-1][g]; steps 1 and 2 then read
  * them from LDS, so their twiddle waits no longer wait for the earlier steps' stores (vmcnt counts
  * loads and stores in one order).  Steps 0 and 3 read the transposed copy from global (TWN 4). */
-constexpr int F45_DMA_SLOTS = 4;
+/* TWN 6: the same for steps 1-3 (a fifth block, A's jj = 3, behind the first four: the image
+ * region grows to 5 x 7 x 225 x 16 B = 126000 B and the stage-twiddle copy moves behind it) */
 __device__ __forceinline__ void glds16(const double2 *g, double2 *lds_base);
-template <int P, int TPG>
+template <int P, int TPG, int NSLOT>
 __device__ __forceinline__ void f45_tw_dma(const double2 *twt, double2 *img, int jt)
 {
-    constexpr int G45 = P / 56, L5 = 7 * G45, NE = F45_DMA_SLOTS * 7 * G45, NW = TPG / 64;
-    static_assert(NE * 16 <= P * 8, "the DMA'd twiddles fit the exchange image");
+    constexpr int G45 = P / 56, L5 = 7 * G45, NE = NSLOT * 7 * G45, NW = TPG / 64;
     const int lane = jt & 63;
     const int wave = __builtin_amdgcn_readfirstlane(jt >> 6);
 #pragma unroll 1
     for (int e0 = wave * 64; e0 < NE; e0 += NW * 64) { /* e0 wave-uniform: the LDS-DMA base */
         const int e = e0 + lane, ec = e < NE ? e : NE - 1;
         const int slot = ec / (7 * G45), r = ec % (7 * G45), i = r / G45, g = r % G45;
-        const int jj = slot < 2 ? slot + 1 : slot + 3; /* slots 0, 1: A's jj = 1, 2; 2, 3: B's jj = 5, 6 */
+        const int jj = slot < 2 ? slot + 1 : slot < 4 ? slot + 3 : 3; /* 0, 1: A's jj 1, 2; 2, 3: B's 5, 6; 4: A's 3 */
         if (e < NE) glds16(twt + i * L5 + jj * G45 + g, img + e0);
     }
     asm volatile("" ::: "memory"); /* later loads / stores stay behind the DMA */
@@ -696,7 +696,7 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
     const double2 *twb = tw + (L5 - 1);
 #pragma unroll
     for (int d = 0; d < 4; d++) {
-        if constexpr (TWN == 5) {
+        if constexpr (TWN == 5 || TWN == 6) {
             if (d == 1) { /* this wave's DMA (older than step 0's loads and 8 stores) has landed, */
                 asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); /* then every wave's */
                 __syncthreads();
@@ -728,6 +728,11 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
                 t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
             } else if constexpr (TWN == 5) {
                 if (d == 1 || d == 2) t = timg[((h ? d + 1 : d - 1) * 7 + i - 1) * G45 + g];
+                else t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
+            } else if constexpr (TWN == 6) {
+                /* slots: A d = 1, 2, 3 -> 0, 1, 4; B d = 1, 2 -> 2, 3 (B's idle d = 3 reads slot 1) */
+                const int sl = d == 3 ? (h ? 1 : 4) : (h ? d + 1 : d - 1);
+                if (d >= 1) t = timg[(sl * 7 + i - 1) * G45 + g];
                 else t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
             } else t = pf::ldg(twb, (7 * k + i - 1) * 16u);
             hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
@@ -842,7 +847,8 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     static_assert(!PRE || (F01 && NT % 2 == 0 && 2 * NT * 8 + ROW_PRE_PTS * 16 <= 160 * 1024 &&
                            ROW_PRE_PTS >= 2 * (P / R0) && P * 8 <= ROW_PRE_PTS * 16),
                   "row prefetch layout");
-    constexpr int PG45 = XP > 0 ? XP : P / 56, IMGD = F45 && 56 * PG45 > P ? 56 * PG45 : P; /* image doubles */
+    constexpr int PG45 = XP > 0 ? XP : P / 56, IMG0 = F45 && 56 * PG45 > P ? 56 * PG45 : P;
+    constexpr int IMGD = TWN == 6 && 10 * (P / 8) > IMG0 ? 10 * (P / 8) : IMG0; /* image doubles (TWN 6: 5 x 7 x P/56 x 2) */
     double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + IMGD + (IMGD & 1));
     double *img = PRE ? ldsd + 2 * NT : ldsd;
     const int jt0 = threadIdx.x, sgn = a.sgn;
@@ -930,9 +936,9 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
                 f45_tw_copy<P, TPG>(a.tw, reinterpret_cast<double2 *>(img), ltw + NT, jt);
                 __syncthreads();
             }
-            if constexpr (TWN == 5) {
+            if constexpr (TWN == 5 || TWN == 6) {
                 __syncthreads(); /* every wave has read the image */
-                f45_tw_dma<P, TPG>(a.tw + P, reinterpret_cast<double2 *>(img), jt);
+                f45_tw_dma<P, TPG, TWN == 5 ? 4 : 5>(a.tw + P, reinterpret_cast<double2 *>(img), jt);
             }
             fused45_pair<P, TPG, CONJ, TWN>(xr, xi, ltw, a.tw, out, jt, sgn, reinterpret_cast<const double2 *>(img),
                                             ltw + NT);
@@ -1118,10 +1124,16 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * it: 6.11 vs 5.98 ms (round 4, removed) */
         size_t lds = lds0;
 #ifdef HSFFT_DEV_PROBES
-        /* round 5 A/B: HSFFT_ROW_TWN=5 -- steps 1-2 of the stage-5 twiddles by LDS-DMA into the image */
+        /* round 5 A/B: HSFFT_ROW_TWN=5 -- steps 1-2 of the stage-5 twiddles by LDS-DMA into the image;
+         * 6 -- steps 1-3 (the image region grows to 126000 B) */
         if (f45 && twn4 && etwn && atoi(etwn) == 5)
             fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 5>
                         : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 5>;
+        if (f45 && twn4 && etwn && atoi(etwn) == 6) {
+            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 6>
+                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 6>;
+            lds = (size_t)10 * (P / 8) * sizeof(double) + (size_t)NT * sizeof(double2);
+        }
         /* round 5 A/B: HSFFT_ROW_XP=260 -- the F45 exchange image with a padded pitch (5.741 vs
          * 5.749 ms per 65536 rows: not kept, profiles/r05b_c3_xp_ab_and_cu_mask.txt) */
         if (f45 && twn4 && getenv("HSFFT_ROW_XP") && atoi(getenv("HSFFT_ROW_XP")) == 260) {

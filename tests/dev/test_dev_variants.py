@@ -98,12 +98,12 @@ def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
     assert T.bits_equal(y2, ref)
 
 
-@pytest.mark.parametrize("twn", ["3", "5"])
+@pytest.mark.parametrize("twn", ["3", "5", "6"])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64, 1])
 def test_12600_row_stage5_twiddles_through_lds(twn, sgn, rows, monkeypatch):
-    """TWN 3: steps 1-3 of the stage-5 twiddles copied into LDS through registers per row; TWN 5:
-    steps 1-2 copied by LDS-DMA into the free exchange image (round 5)"""
+    """TWN 3: steps 1-3 of the stage-5 twiddles copied into LDS through registers per row; TWN 5 / 6:
+    steps 1-2 / 1-3 copied by LDS-DMA into the free exchange image (round 5)"""
     monkeypatch.setenv("HSFFT_ROW_TWN", twn)
     n = 12600
     x = T.complex_input(n, 77, batch=rows).reshape(rows, n)
