@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-5 GPU session E: parity of the development build (tests/dev: new c3 row kernel with the
-# stage-5 twiddles of steps 1-2 by LDS-DMA, HSFFT_ROW_TWN=5), then in-process A/B: c3 TWN 5 vs 4;
+# stage-5 twiddles of steps 1-2 / 1-3 by LDS-DMA, HSFFT_ROW_TWN=5 / 6), then in-process A/B: c3 TWN 5, 6 vs 4;
 # c4 with the spill-free k_bxcd: one acquire per iteration (HSFFT_BX_MERGE) and the poll sleep
 # (HSFFT_BX_SLEEP) re-checked.
 set -u
@@ -15,7 +15,7 @@ ab() {
   echo "== $*"; grep -E "median" gpurun_out/r5e_ab_$i.log
   [ $rc = 0 ] || { echo "rc=$rc"; tail -5 gpurun_out/r5e_ab_$i.log; exit $rc; }
 }
-HSFFT_LIB_PATH=$DEV ab --config c3 --var HSFFT_ROW_TWN --values unset,5 --rounds 8 --iters 5
+HSFFT_LIB_PATH=$DEV ab --config c3 --var HSFFT_ROW_TWN --values unset,5,6 --rounds 8 --iters 5
 ab --config c4 --var HSFFT_BX_MERGE --values unset,1 --rounds 5 --iters 3
 ab --config c4 --var HSFFT_BX_SLEEP --values unset,0,4 --rounds 5 --iters 3
 exit 0
