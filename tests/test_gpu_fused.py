@@ -198,6 +198,31 @@ def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
     assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
 
 
+@pytest.mark.parametrize("ng,batch,jitter", [("8", 19, "0"), ("3", 7, "5"), ("8", 1, "0")])
+@pytest.mark.parametrize("n", [99991, 65537, 131071])
+def test_bluestein_persistent_unconditional_loads(n, ng, batch, jitter, monkeypatch):
+    """k_bxcd<S, UL = true> (HSFFT_BX_UL=1, round 5): P1's row / chirp loads and P3's chirp loads
+    issued unconditionally at clamped indices, the padding and the n < N store condition applied
+    to the values -- bit-exact vs the oracle, both signs, uneven load"""
+    monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
+    monkeypatch.setenv("HSFFT_BX_JITTER", jitter)
+    monkeypatch.setenv("HSFFT_BX_UL", "1")
+    fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
+    x = T.complex_input(n, 0xB8 ^ n ^ batch, batch=batch).reshape(batch, n)
+    for sgn in (1, -1):
+        p = hsfft.Plan(n, sgn)
+        din = hsfft.DeviceBuffer.from_array(x)
+        dout = hsfft.DeviceBuffer(x.nbytes)
+        hsfft.exec_batched(p, din, dout, batch)
+        hsfft.synchronize()
+        y = dout.to_array(np.complex128).reshape(batch, n)
+        assert T.bits_equal(y, _oracle(x, sgn, ("bxul", n, batch))), (n, sgn, ng, batch)
+        din.free()
+        dout.free()
+        p.close()
+    assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
+
+
 @pytest.mark.parametrize("mode", ["refused", "refused_coop", "sync"])
 def test_bluestein_persistent_launch_contract(mode, monkeypatch):
     """The persistent Bluestein launch needs every workgroup resident at once.  refused: 9
