@@ -41,7 +41,7 @@ BUDGETS = [
     # persistent Bluestein (c4): the whole grid (2 workgroups per CU) must be resident, so
     # 128 VGPRs is a hard limit; round 4's 8 dwords of spill went away in round 5 (the wait
     # bound became a kernel argument: 127 VGPRs, no spill)
-    (r"^_ZN3bxc6k_bxcdILin?1EE", 0, 128, 4),
+    (r"^_ZN3bxc6k_bxcdILin?1ELb[01]EE", 0, 128, 4),
 ]
 
 
