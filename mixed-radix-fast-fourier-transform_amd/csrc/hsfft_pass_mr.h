@@ -576,17 +576,14 @@ __device__ __forceinline__ double lane_swap(double v)
 }
 
 /* exchange fused_ab's outputs (as xchg1_ab_std writes them) into F45's stage-4 inputs: thread
- * (g, h) reads butterflies ml = 4h + c (c < 4) at kloc = g, point i at (ml + 8i)*PITCH + g.
- * The image is [56][PITCH] doubles.  PITCH = G45 (225) is the packed layout; a padded pitch
- * with PITCH % 8 == 4 (260) puts the rows of thread A (h = 0) and thread B (h = 1) of one
- * 32-lane ds_read_b64 group 32 banks apart (4 rows = 8*PITCH dwords = 32 mod 64), and steps c
- * 2080 B apart, beyond ds_read2_b64's offset range: every read a conflict-free ds_read_b64 */
-template <int RA, int RB, int L, int P, int TPG, int PITCH = P / 56>
+ * (g, h) reads butterflies ml = 4h + c (c < 4) at kloc = g, point i at (ml + 8i)*G45 + g.
+ * (A padded pitch of 260 doubles, conflict-free ds_read_b64 instead of ds_read2_b64, measured
+ * 5.741 vs 5.749 ms in round 5 and removed.) */
+template <int RA, int RB, int L, int P, int TPG>
 __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 {
     constexpr int Q = RA * RB, NG2 = P / Q, NGT = cdiv(NG2, TPG), LN = L * Q, G45 = P / 56;
     static_assert(LN == G45, "F45 follows F23 at L = P / 56");
-    static_assert(PITCH >= G45, "F45 image pitch");
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < NGT; c++) {
@@ -596,7 +593,7 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 #pragma unroll
         for (int jj = 0; jj < RA; jj++)
 #pragma unroll
-            for (int jq = 0; jq < RB; jq++) ld[mlp * PITCH + kloc + jj * L + jq * L * RA] = x[c * Q + jj * RB + jq];
+            for (int jq = 0; jq < RB; jq++) ld[mlp * LN + kloc + jj * L + jq * L * RA] = x[c * Q + jj * RB + jq];
     }
     __syncthreads();
     const int h = jt & 1;
@@ -605,7 +602,7 @@ __device__ __forceinline__ void xchg1_ab_g45(double *x, double *ld, int jt)
 #pragma unroll
     for (int c = 0; c < 4; c++)
 #pragma unroll
-        for (int i = 0; i < 7; i++) x[c * 7 + i] = ld[(4 * h + c + 8 * i) * PITCH + g];
+        for (int i = 0; i < 7; i++) x[c * 7 + i] = ld[(4 * h + c + 8 * i) * G45 + g];
 }
 
 /* TWN 3: the stage-5 twiddles of steps d >= 1 (k-blocks jj = 1, 2, 3 of thread A and 5, 6 of
@@ -640,31 +637,6 @@ __device__ __forceinline__ void f45_tw_copy(const double2 *tw, double2 *img, dou
     }
 }
 
-/* TWN 5: the stage-5 twiddles of steps 1 and 2 (k-blocks jj = 1, 2 of thread A and 5, 6 of thread
- * B: 4 blocks x 7 x 225 entries = 100800 B, exactly the exchange image) copied by LDS-DMA from the
- * plan's transposed copy (tw + P, [i-1][k]) into the free exchange image right after the last
- * exchange's reads -- before any store of the row -- as [slot][i-1][g]; steps 1 and 2 then read
- * them from LDS, so their twiddle waits no longer wait for the earlier steps' stores (vmcnt counts
- * loads and stores in one order).  Steps 0 and 3 read the transposed copy from global (TWN 4). */
-/* TWN 6: the same for steps 1-3 (a fifth block, A's jj = 3, behind the first four: the image
- * region grows to 5 x 7 x 225 x 16 B = 126000 B and the stage-twiddle copy moves behind it) */
-__device__ __forceinline__ void glds16(const double2 *g, double2 *lds_base);
-template <int P, int TPG, int NSLOT>
-__device__ __forceinline__ void f45_tw_dma(const double2 *twt, double2 *img, int jt)
-{
-    constexpr int G45 = P / 56, L5 = 7 * G45, NE = NSLOT * 7 * G45, NW = TPG / 64;
-    const int lane = jt & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(jt >> 6);
-#pragma unroll 1
-    for (int e0 = wave * 64; e0 < NE; e0 += NW * 64) { /* e0 wave-uniform: the LDS-DMA base */
-        const int e = e0 + lane, ec = e < NE ? e : NE - 1;
-        const int slot = ec / (7 * G45), r = ec % (7 * G45), i = r / G45, g = r % G45;
-        const int jj = slot < 2 ? slot + 1 : slot < 4 ? slot + 3 : 3; /* 0, 1: A's jj 1, 2; 2, 3: B's 5, 6; 4: A's 3 */
-        if (e < NE) glds16(twt + i * L5 + jj * G45 + g, img + e0);
-    }
-    asm volatile("" ::: "memory"); /* later loads / stores stay behind the DMA */
-}
-
 /* stages 4 (radix 7) and 5 (radix 8) of the pair's group, then the row's stores */
 template <int P, int TPG, bool CONJ, int TWN = 0>
 __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const double2 *ltw, const double2 *tw,
@@ -696,12 +668,6 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
     const double2 *twb = tw + (L5 - 1);
 #pragma unroll
     for (int d = 0; d < 4; d++) {
-        if constexpr (TWN == 5 || TWN == 6) {
-            if (d == 1) { /* this wave's DMA (older than step 0's loads and 8 stores) has landed, */
-                asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); /* then every wave's */
-                __syncthreads();
-            }
-        }
         const int jj = h ? 4 + d : d, da = d < 3 ? 4 + d : 6;
         double zr[8], zi[8];
 #pragma unroll
@@ -726,14 +692,6 @@ __device__ __forceinline__ void fused45_pair(double *xr, double *xi, const doubl
             } else if constexpr (TWN == 4) {
                 /* the plan's transposed copy of this stage's block at tw + P ([i-1][k]) */
                 t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
-            } else if constexpr (TWN == 5) {
-                if (d == 1 || d == 2) t = timg[((h ? d + 1 : d - 1) * 7 + i - 1) * G45 + g];
-                else t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
-            } else if constexpr (TWN == 6) {
-                /* slots: A d = 1, 2, 3 -> 0, 1, 4; B d = 1, 2 -> 2, 3 (B's idle d = 3 reads slot 1) */
-                const int sl = d == 3 ? (h ? 1 : 4) : (h ? d + 1 : d - 1);
-                if (d >= 1) t = timg[(sl * 7 + i - 1) * G45 + g];
-                else t = pf::ldg(tw + P, ((i - 1) * L5 + k) * 16u);
             } else t = pf::ldg(twb, (7 * k + i - 1) * 16u);
             hsb::twmul(zr[i], zi[i], t.x, CONJ ? -t.y : t.y);
         }
@@ -829,9 +787,8 @@ constexpr int ROW_PRE_PTS = 8448;
 /* PF: the inputs of the next row's first PF 9-point groups (37 % of a row per group at
  * TPG = 512) are loaded into registers right after this row's first exchange, so their
  * latency overlaps this row's remaining stages (needs the VGPRs of TPG = 512: 256 per thread) */
-/* XP (F45): the pitch of the F45 exchange image in doubles (0: packed, P/56) -- xchg1_ab_g45 */
 template <int R0, int R1, int R2, int R3, int R4, int R5, int TPG, bool CONJ, bool F01, bool PRE = false, int PF = 0,
-          bool F23 = false, bool F45 = false, int TWN = 0, int XP = 0>
+          bool F23 = false, bool F45 = false, int TWN = 0>
 __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
 {
     static_assert(!F45 || (F23 && R4 == 7 && R5 == 8 && 2 * (R0 * R1 * R2 * R3) <= TPG), "F45: [7,8] after F23");
@@ -847,9 +804,7 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
     static_assert(!PRE || (F01 && NT % 2 == 0 && 2 * NT * 8 + ROW_PRE_PTS * 16 <= 160 * 1024 &&
                            ROW_PRE_PTS >= 2 * (P / R0) && P * 8 <= ROW_PRE_PTS * 16),
                   "row prefetch layout");
-    constexpr int PG45 = XP > 0 ? XP : P / 56, IMG0 = F45 && 56 * PG45 > P ? 56 * PG45 : P;
-    constexpr int IMGD = TWN == 6 && 10 * (P / 8) > IMG0 ? 10 * (P / 8) : IMG0; /* image doubles (TWN 6: 5 x 7 x P/56 x 2) */
-    double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + IMGD + (IMGD & 1));
+    double2 *ltw = PRE ? reinterpret_cast<double2 *>(ldsd) : reinterpret_cast<double2 *>(ldsd + P + (P & 1));
     double *img = PRE ? ldsd + 2 * NT : ldsd;
     const int jt0 = threadIdx.x, sgn = a.sgn;
     /* LDS copy of the stage-1..4 twiddles, transposed within each stage's block [L-1, RL-1):
@@ -928,17 +883,13 @@ __global__ __launch_bounds__(TPG) void k_row2(MArgs a)
         if constexpr (F45) { /* stages 2-3 fused, then 4-5 fused over thread pairs: two exchanges */
             fused_ab<R2, R3, LS::Lloc(2), P, TPG, CONJ>(xr, xi, ltw, jt, sgn);
             mark(a, tp, 2);
-            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG, PG45>(xr, img, jt);
-            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG, PG45>(xi, img, jt);
+            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xr, img, jt);
+            xchg1_ab_g45<R2, R3, LS::Lloc(2), P, TPG>(xi, img, jt);
             mark(a, tp, 3);
             if constexpr (TWN == 3) {
                 __syncthreads(); /* every wave has read the image */
                 f45_tw_copy<P, TPG>(a.tw, reinterpret_cast<double2 *>(img), ltw + NT, jt);
                 __syncthreads();
-            }
-            if constexpr (TWN == 5 || TWN == 6) {
-                __syncthreads(); /* every wave has read the image */
-                f45_tw_dma<P, TPG, TWN == 5 ? 4 : 5>(a.tw + P, reinterpret_cast<double2 *>(img), jt);
             }
             fused45_pair<P, TPG, CONJ, TWN>(xr, xi, ltw, a.tw, out, jt, sgn, reinterpret_cast<const double2 *>(img),
                                             ltw + NT);
@@ -1124,23 +1075,10 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
          * it: 6.11 vs 5.98 ms (round 4, removed) */
         size_t lds = lds0;
 #ifdef HSFFT_DEV_PROBES
-        /* round 5 A/B: HSFFT_ROW_TWN=5 -- steps 1-2 of the stage-5 twiddles by LDS-DMA into the image;
-         * 6 -- steps 1-3 (the image region grows to 126000 B) */
-        if (f45 && twn4 && etwn && atoi(etwn) == 5)
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 5>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 5>;
-        if (f45 && twn4 && etwn && atoi(etwn) == 6) {
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 6>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 6>;
-            lds = (size_t)10 * (P / 8) * sizeof(double) + (size_t)NT * sizeof(double2);
-        }
-        /* round 5 A/B: HSFFT_ROW_XP=260 -- the F45 exchange image with a padded pitch (5.741 vs
-         * 5.749 ms per 65536 rows: not kept, profiles/r05b_c3_xp_ab_and_cu_mask.txt) */
-        if (f45 && twn4 && getenv("HSFFT_ROW_XP") && atoi(getenv("HSFFT_ROW_XP")) == 260) {
-            fn = a.conj ? k_row2<3, 3, 5, 5, 7, 8, 512, true, true, false, 1, true, true, 4, 260>
-                        : k_row2<3, 3, 5, 5, 7, 8, 512, false, true, false, 1, true, true, 4, 260>;
-            lds = (size_t)56 * 260 * sizeof(double) + (size_t)NT * sizeof(double2);
-        }
+        /* round 5, measured and removed: the stage-5 twiddles of steps 1-2 / 1-3 copied by LDS-DMA
+         * into the free exchange image before the row's stores, 5.83 / 6.17 vs 5.68 ms
+         * (profiles/r05e_c3_twn_c4_ul_ab.txt); the F45 exchange image with a padded pitch (no bank
+         * conflicts, no ds_read2_b64), 5.741 vs 5.749 ms (profiles/r05b_c3_xp_ab_and_cu_mask.txt) */
         /* development build only (measurement): HSFFT_ROW_TWN=2 constant stage-5 twiddles, results
          * wrong (5.46-5.49 ms: what the twiddle loads cost); 3 those of steps 1-3 copied into LDS
          * before the row's stores (6.20 vs 5.89 ms).  Loading step d+1's run before step d's

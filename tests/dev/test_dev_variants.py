@@ -12,8 +12,7 @@ Variants: pf::k_r2c_walk2 (round 3's one-per-CU split walk; HSFFT_R2C_WALK=2) wi
 lengths and orders; k_r2c_walk1's other prefetch forms (HSFFT_R2C_PFH 0 / 2 / 3) and walk
 orders (HSFFT_R2C_ORDER); round 1's split kernel r8::k_r2c_last (HSFFT_R2C_FUSE=2); pass A and
 the split walk overlapped over sub-chunks (HSFFT_R2C_OVL); the c3 row kernel's stage-5 twiddles
-of steps 1-3 through LDS (HSFFT_ROW_TWN=3) or of steps 1-2 by LDS-DMA (=5), its F45 exchange image
-with a padded pitch (HSFFT_ROW_XP=260).  Bit-exact vs the oracle.
+of steps 1-3 through LDS (HSFFT_ROW_TWN=3).  Bit-exact vs the oracle.
 """
 import numpy as np
 import pytest
@@ -98,28 +97,13 @@ def test_r2c_overlapped_subchunks(n, batch, ovl, monkeypatch):
     assert T.bits_equal(y2, ref)
 
 
-@pytest.mark.parametrize("twn", ["3", "5", "6"])
 @pytest.mark.parametrize("sgn", [1, -1])
 @pytest.mark.parametrize("rows", [300, 64, 1])
-def test_12600_row_stage5_twiddles_through_lds(twn, sgn, rows, monkeypatch):
-    """TWN 3: steps 1-3 of the stage-5 twiddles copied into LDS through registers per row; TWN 5 / 6:
-    steps 1-2 / 1-3 copied by LDS-DMA into the free exchange image (round 5)"""
-    monkeypatch.setenv("HSFFT_ROW_TWN", twn)
+def test_12600_row_stage5_twiddles_through_lds(sgn, rows, monkeypatch):
+    """TWN 3: steps 1-3 of the stage-5 twiddles copied into LDS through registers per row"""
+    monkeypatch.setenv("HSFFT_ROW_TWN", "3")
     n = 12600
     x = T.complex_input(n, 77, batch=rows).reshape(rows, n)
-    p = hsfft.Plan(n, sgn)
-    din = hsfft.DeviceBuffer.from_array(x)
-    dout = hsfft.DeviceBuffer(x.nbytes)
-    hsfft.exec_batched(p, din, dout, rows)
-    y = dout.to_array(np.complex128).reshape(rows, n)
-    assert T.bits_equal(y, T.oracle_c2c(x, sgn))
-
-
-@pytest.mark.parametrize("sgn", [1, -1])
-def test_12600_row_padded_f45_pitch(sgn, monkeypatch):
-    monkeypatch.setenv("HSFFT_ROW_XP", "260")
-    n, rows = 12600, 300
-    x = T.complex_input(n, 79, batch=rows).reshape(rows, n)
     p = hsfft.Plan(n, sgn)
     din = hsfft.DeviceBuffer.from_array(x)
     dout = hsfft.DeviceBuffer(x.nbytes)
