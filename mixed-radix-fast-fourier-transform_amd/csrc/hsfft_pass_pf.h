@@ -795,10 +795,25 @@ __device__ __forceinline__ void w1_stages(double (&xr)[8], double (&xi)[8], doub
     p_stage<PROBE, SGN>(xr, xi, w);
 }
 
+#ifdef HSFFT_DEV_PROBES
+/* this workgroup's CU: XCD, shader engine, shader array and CU fields of HW_ID (< 2048) */
+__device__ __forceinline__ unsigned cu_slot()
+{
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));   /* HW_REG_HW_ID */
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11)); /* HW_REG_XCC_ID */
+    return ((xcc & 7) << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
+}
+#endif
+
 /* PFH: the next tile's hi rows are loaded at the start of this tile's pairs phase, i.e. before
  * its store burst, so waiting for them does not wait for the stores (vmcnt is in order); PFL:
- * the lo rows are loaded at the start of the hi phase, while the hi tile is transformed */
-template <int SGN, bool PFH = false, bool PFL = false, int PROBE = 0>
+ * the lo rows are loaded at the start of the hi phase, while the hi tile is transformed.
+ * STOK (development build, round 5 -- the test of the store-burst alignment hypothesis): the
+ * two walks a CU holds never have store bursts in flight together.  A per-CU token word
+ * (a.dbg[cu_slot()], zero when free) is taken by thread 0 before the pairs phase and returned
+ * once the phase's stores have drained (1) or once they are issued (2); the wait is bounded
+ * (50 us, about one tile pair), after which the walk stores without the token */
+template <int SGN, bool PFH = false, bool PFL = false, int PROBE = 0, int STOK = 0>
 __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsigned T, unsigned W)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -896,6 +911,36 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
         for (int jj = 0; jj < 8; jj++) ld[(jt + jj * TPG) * G + g] = him[jj];
         __syncthreads();
         /* ---- pairs: X[N-k], X[h-k] aligned; X[k], X[h+k] shifted one lane onto line [8j, 8j+8) */
+#ifdef HSFFT_DEV_PROBES
+        bool own = false;
+        unsigned *tok = nullptr;
+        if constexpr (STOK != 0) {
+            tok = a.dbg + cu_slot();
+            if (tid0 == 0) {
+                const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+                unsigned tries = 0;
+                for (;; tries++) {
+                    if (atomicCAS(tok, 0u, blockIdx.x + 1u) == 0u) {
+                        own = true;
+                        break;
+                    }
+                    if ((unsigned)__builtin_amdgcn_s_memrealtime() - t0 > 5000u) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                /* statistics after the 2048 token words: pairs phases, phases that waited, timeouts,
+                 * 10-ns ticks waited */
+                if (a.tiles_q) {
+                    atomicAdd(a.dbg + 2048, 1u);
+                    if (tries) {
+                        atomicAdd(a.dbg + 2049, 1u);
+                        atomicAdd(a.dbg + 2051, (unsigned)__builtin_amdgcn_s_memrealtime() - t0);
+                    }
+                    if (!own) atomicAdd(a.dbg + 2050, 1u);
+                }
+            }
+            __syncthreads();
+        }
+#endif
         if constexpr (PFH) { /* unconditional: the last tile reloads itself */
             const unsigned jn = jr + 1 < len ? j0 + (o + jr + 1) % len : j;
             w1_rows(pr, pi, row, B, B - 8 * jn - 8, tid);
@@ -935,6 +980,13 @@ __global__ __launch_bounds__(512, 4) void k_r2c_walk1(Args a, unsigned h, unsign
                 cry[512 + u] = vb;
             }
         }
+#ifdef HSFFT_DEV_PROBES
+        if constexpr (STOK != 0) {
+            if constexpr (STOK == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid0 == 0 && own) atomicCAS(tok, blockIdx.x + 1u, 0u);
+        }
+#endif
     }
     const unsigned jend = o > 0 ? j0 + o : j1;
     if (len > 0 && jend < B / 16 && (tid0 & 7) == 0) {
@@ -1001,7 +1053,7 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         wfn fw = sgn == 1 ? k_r2c_walk1<1, true> : k_r2c_walk1<-1, true>;
         int lds_bytes = R2CW1_LDS;
         a.tile_major = 9; /* 8 rotation classes */
-        bool dbg = false;
+        bool dbg = false, stok_stats = false;
 #ifdef HSFFT_DEV_PROBES
         {
             /* development build: HSFFT_R2C_WALK=2 k_r2c_walk2 (round 3's one-per-CU walk, walks of
@@ -1036,6 +1088,20 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
                 case 31: fw = k_r2c_walk1<1, true, false, 31>; break;
                 default: break;
                 }
+                /* HSFFT_R2C_STOK 1 / 2: the per-CU store token (see k_r2c_walk1), bit-exact */
+                const int stok = env("HSFFT_R2C_STOK", 0);
+                if (stok == 1 || stok == 2) {
+                    static unsigned *s_tok = nullptr;
+                    if (!s_tok) {
+                        HCHK(hipMalloc((void **)&s_tok, 2052 * sizeof(unsigned)));
+                        HCHK(hipMemset(s_tok, 0, 2052 * sizeof(unsigned)));
+                    }
+                    a.dbg = s_tok;
+                    stok_stats = env("HSFFT_R2C_STOK_STATS", 0) != 0;
+                    a.tiles_q = stok_stats ? 1 : 0; /* walk1 does not read tiles_q otherwise */
+                    fw = stok == 1 ? (sgn == 1 ? k_r2c_walk1<1, true, false, 0, 1> : k_r2c_walk1<-1, true, false, 0, 1>)
+                                   : (sgn == 1 ? k_r2c_walk1<1, true, false, 0, 2> : k_r2c_walk1<-1, true, false, 0, 2>);
+                }
             }
             /* walk orders: 0 row-major, 1 segment-major, 2 rotated, >= 3 rotation classes */
             a.tile_major = env("HSFFT_R2C_ORDER", 9);
@@ -1055,6 +1121,14 @@ inline int launch_r2c_fused(const void *Z, long long zdist, void *X, long long x
         HCHK(hipFuncSetAttribute((const void *)fw, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
         hipLaunchKernelGGL(fw, dim3((unsigned)grid), dim3(512), lds_bytes, st, a, (unsigned)h, (unsigned)T, (unsigned)W);
         HCHK(hipGetLastError());
+        if (stok_stats) { /* development build: the store token's statistics of this launch */
+            unsigned hs[4];
+            HCHK(hipMemcpyAsync(hs, a.dbg + 2048, sizeof hs, hipMemcpyDeviceToHost, st));
+            HCHK(hipStreamSynchronize(st));
+            HCHK(hipMemsetAsync(a.dbg + 2048, 0, sizeof hs, st));
+            fprintf(stderr, "r2c store token: %u pairs phases, %u waited (mean %.2f us), %u timed out\n", hs[0], hs[1],
+                    hs[1] ? hs[3] / 100.0 / hs[1] : 0.0, hs[2]);
+        }
         if (dbg) { /* mean us per tile pair of the walking workgroups */
             unsigned *hb = (unsigned *)malloc((size_t)grid * 4 * sizeof(unsigned));
             if (!hb) return -1;

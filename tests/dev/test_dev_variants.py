@@ -10,7 +10,7 @@ Collected only with HSFFT_DEV_TESTS=1 and HSFFT_LIB_PATH pointing at the develop
 
 Variants: pf::k_r2c_walk2 (round 3's one-per-CU split walk; HSFFT_R2C_WALK=2) with its walk
 lengths and orders; k_r2c_walk1's other prefetch forms (HSFFT_R2C_PFH 0 / 2 / 3) and walk
-orders (HSFFT_R2C_ORDER); round 1's split kernel r8::k_r2c_last (HSFFT_R2C_FUSE=2); pass A and
+orders (HSFFT_R2C_ORDER) and its per-CU store token (HSFFT_R2C_STOK); round 1's split kernel r8::k_r2c_last (HSFFT_R2C_FUSE=2); pass A and
 the split walk overlapped over sub-chunks (HSFFT_R2C_OVL); the c3 row kernel's stage-5 twiddles
 of steps 1-3 through LDS (HSFFT_ROW_TWN=3).  Bit-exact vs the oracle.
 """
@@ -110,3 +110,13 @@ def test_12600_row_stage5_twiddles_through_lds(sgn, rows, monkeypatch):
     hsfft.exec_batched(p, din, dout, rows)
     y = dout.to_array(np.complex128).reshape(rows, n)
     assert T.bits_equal(y, T.oracle_c2c(x, sgn))
+
+
+@pytest.mark.parametrize("stok", ["1", "2"])
+@pytest.mark.parametrize("n,sgn,batch", [(1 << 22, 1, 3), (1 << 19, 1, 300), (1 << 17, -1, 5)])
+def test_r2c_walk1_store_token(n, sgn, batch, stok, monkeypatch):
+    """round 5: the per-CU store token (HSFFT_R2C_STOK) only delays a walk's pairs phase; 2^19 x
+    300 rows puts 600 walks on 256 CUs, so two walks share a CU and contend for the token"""
+    monkeypatch.setenv("HSFFT_R2C_STOK", stok)
+    y, ref = _r2c(n, sgn, batch, 37)
+    assert T.bits_equal(y, ref)

@@ -30,7 +30,7 @@ BUDGETS = [
     (r"^_ZN2pf8k_firstqILi8ELi3ELi1ELin?1ELb[01]ELb[01]EE", 0, 128, 4),
     # r2c split walk (c5, default since round 4: the next hi tile's rows loaded before the
     # stores): two 512-thread workgroups per CU, 128 VGPRs, no spill
-    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0EE", 0, 128, 4),
+    (r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0ELi0EE", 0, 128, 4),
     # 12600 row kernel (c3, default since round 4: stages 4-5 fused over thread pairs,
     # HSFFT_ROW_F45=1, stage-5 twiddles from the transposed copy, HSFFT_ROW_TWN=4; the other
     # twiddle variants beside it): one 512-thread workgroup per CU
@@ -117,7 +117,9 @@ def test_no_wrong_result_probes_in_product():
                   b"HSFFT_R2C_W1PROBE",
                   # measured slower (round 4): the two-stream r2c overlap, walk1's other prefetch
                   # forms and walk orders, walk2's phase trace
-                  b"HSFFT_R2C_OVL", b"HSFFT_R2C_PFH", b"HSFFT_R2C_ORDER", b"HSFFT_R2C_DEBUG"):
+                  b"HSFFT_R2C_OVL", b"HSFFT_R2C_PFH", b"HSFFT_R2C_ORDER", b"HSFFT_R2C_DEBUG",
+                  # round 5's per-CU store token (the store-burst alignment test)
+                  b"HSFFT_R2C_STOK"):
         assert probe not in blob, probe
     names = _metadata()
     bad = [k for k in names
@@ -126,7 +128,7 @@ def test_no_wrong_result_probes_in_product():
            or re.match(r"^_ZN2mr6k_row2I.*ELi2EEEvNS_5MArgsE$", k)
            # measured slower: walk1's other prefetch forms, the one-per-CU walk2, round 1's split
            # kernel r8::k_r2c_last, the c3 row kernel's stage-5 twiddles through LDS (TWN = 3)
-           or (re.match(r"^_ZN2pf11k_r2c_walk1", k) and not re.match(r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0EE", k))
+           or (re.match(r"^_ZN2pf11k_r2c_walk1", k) and not re.match(r"^_ZN2pf11k_r2c_walk1ILin?1ELb1ELb0ELi0ELi0EE", k))
            or re.match(r"^_ZN2pf11k_r2c_walk2", k)
            or re.match(r"^_ZN2r810k_r2c_last", k)
            or re.match(r"^_ZN2mr6k_row2I.*ELi3EEEvNS_5MArgsE$", k)]
