@@ -156,13 +156,14 @@ __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned targ
     return (st & 1) == 0;
 }
 
-/* UL (round 5): every load of P1 (input row, chirp) and P3 (chirp) is issued unconditionally at a
+/* Round 5: every load of P1 (input row, chirp) and P3 (chirp) is issued unconditionally at a
  * clamped index, the zero padding / the n < N store condition applied to the VALUES -- with the
  * n < nsig test around the loads hipcc branched around each one and waited vmcnt(0) after it
  * (cdna_hip_programming.md, the per-element "register or load" trap): P3's eight chirp loads
  * each waited for the previous element's store, P1's row loads one by one.  Same arithmetic on
- * the same values: bit-identical. */
-template <int S, bool UL = false>
+ * the same values (bit-identical); in-process A/B on two boxes 32.40 vs 32.62 and 32.08 vs 32.35
+ * ms per 8192 rows (profiles/r05e_*, r05f_*). */
+template <int S>
 __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -266,26 +267,19 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
             for (int i = 0; i < 7; i++) w[i] = make_double2(w2[i].x, -w2[i].y);
             pf::stage<8, -S>(xr, xi, w, false);
             double2 *orow = a.out + (long long)(grp + (k - 2) * ng) * a.odist;
-            if constexpr (UL) { /* the chirp values of four outputs at a time, loaded together */
+            /* the chirp values of four outputs at a time, loaded together */
 #pragma unroll
-                for (int h4 = 0; h4 < 8; h4 += 4) {
-                    double2 ch[4];
+            for (int h4 = 0; h4 < 8; h4 += 4) {
+                double2 ch[4];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const unsigned n = (jt + (h4 + u) * TPG) * B + q;
-                        ch[u] = a.chirp[n < nsig ? n : nsig - 1];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const unsigned n = (jt + (h4 + u) * TPG) * B + q;
-                        if (n < nsig) orow[n] = bpf::chirp_out<S>(xr[h4 + u], xi[h4 + u], ch[u]);
-                    }
+                for (int u = 0; u < 4; u++) {
+                    const unsigned n = (jt + (h4 + u) * TPG) * B + q;
+                    ch[u] = a.chirp[n < nsig ? n : nsig - 1];
                 }
-            } else {
 #pragma unroll
-                for (int jj = 0; jj < 8; jj++) {
-                    const unsigned n = (jt + jj * TPG) * B + q;
-                    if (n < nsig) orow[n] = bpf::chirp_out<S>(xr[jj], xi[jj], a.chirp[n]);
+                for (int u = 0; u < 4; u++) {
+                    const unsigned n = (jt + (h4 + u) * TPG) * B + q;
+                    if (n < nsig) orow[n] = bpf::chirp_out<S>(xr[h4 + u], xi[h4 + u], ch[u]);
                 }
             }
             BX_MARK(5)
@@ -350,42 +344,25 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
                 const unsigned n = (jt + i * TPG) * A + q;
                 hin[i] = a.chirp[n < nsig ? n : 0];
             }
-            if constexpr (UL) { /* every row load issued, the padding applied to the values */
-                double2 x4[4];
+            /* every row load issued, the padding applied to the values */
+            double2 x4[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const unsigned n = (jt + i * TPG) * A + q;
-                    x4[i] = row[n < nsig ? n : nsig - 1];
-                }
+            for (int i = 0; i < 4; i++) {
+                const unsigned n = (jt + i * TPG) * A + q;
+                x4[i] = row[n < nsig ? n : nsig - 1];
+            }
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const unsigned n = (jt + i * TPG) * A + q;
-                    const double2 x = x4[i];
-                    double2 v;
-                    if (S == 1) v = make_double2(x.x * hin[i].x + x.y * hin[i].y, -x.x * hin[i].y + x.y * hin[i].x);
-                    else v = make_double2(x.x * hin[i].x - x.y * hin[i].y, x.x * hin[i].y + x.y * hin[i].x);
-                    const bool inside = n < nsig;
-                    xr[i] = inside ? v.x : 0.0;
-                    xi[i] = inside ? v.y : 0.0;
-                    xr[i + 4] = 0.0;
-                    xi[i + 4] = 0.0;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const unsigned n = (jt + i * TPG) * A + q;
-                    const bool inside = n < nsig;
-                    const double2 x = row[inside ? n : 0];
-                    double2 v = make_double2(0.0, 0.0);
-                    if (inside) {
-                        if (S == 1) v = make_double2(x.x * hin[i].x + x.y * hin[i].y, -x.x * hin[i].y + x.y * hin[i].x);
-                        else v = make_double2(x.x * hin[i].x - x.y * hin[i].y, x.x * hin[i].y + x.y * hin[i].x);
-                    }
-                    xr[i] = v.x;
-                    xi[i] = v.y;
-                    xr[i + 4] = 0.0;
-                    xi[i + 4] = 0.0;
-                }
+            for (int i = 0; i < 4; i++) {
+                const unsigned n = (jt + i * TPG) * A + q;
+                const double2 x = x4[i];
+                double2 v;
+                if (S == 1) v = make_double2(x.x * hin[i].x + x.y * hin[i].y, -x.x * hin[i].y + x.y * hin[i].x);
+                else v = make_double2(x.x * hin[i].x - x.y * hin[i].y, x.x * hin[i].y + x.y * hin[i].x);
+                const bool inside = n < nsig;
+                xr[i] = inside ? v.x : 0.0;
+                xi[i] = inside ? v.y : 0.0;
+                xr[i + 4] = 0.0;
+                xi[i + 4] = 0.0;
             }
             pf::stage<8, S>(xr, xi, w, true);
             r8::exchange<8, 1, 8, TPG, P, G, false>(xr, xi, lds, jt, g);

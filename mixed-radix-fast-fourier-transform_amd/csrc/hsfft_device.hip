@@ -768,11 +768,6 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         img_bytes < (size_t)ng * bxc::NIMG * bxc::IMG * sizeof(double2))
         return 1;
     void (*fn)(bxc::XArgs) = sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>;
-    {
-        /* round 5 A/B: HSFFT_BX_UL=1 -- P1 / P3 loads unconditional (bxc::k_bxcd UL) */
-        const char *ue = getenv("HSFFT_BX_UL");
-        if (ue && atoi(ue)) fn = sgn == 1 ? bxc::k_bxcd<1, true> : bxc::k_bxcd<-1, true>;
-    }
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bxc::LDS_BYTES));
     const int grid = ng * (int)bxc::NTILE;
     const char *ce = getenv("HSFFT_BX_COOP");

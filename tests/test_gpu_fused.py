@@ -201,12 +201,12 @@ def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
 @pytest.mark.parametrize("ng,batch,jitter", [("8", 19, "0"), ("3", 7, "5"), ("8", 1, "0")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
 def test_bluestein_persistent_unconditional_loads(n, ng, batch, jitter, monkeypatch):
-    """k_bxcd<S, UL = true> (HSFFT_BX_UL=1, round 5): P1's row / chirp loads and P3's chirp loads
-    issued unconditionally at clamped indices, the padding and the n < N store condition applied
-    to the values -- bit-exact vs the oracle, both signs, uneven load"""
+    """k_bxcd's loads (round 5): P1's row / chirp loads and P3's chirp loads issued
+    unconditionally at clamped indices, the padding and the n < N store condition applied to
+    the values -- bit-exact vs the oracle at lengths whose last tile is partly padding, both
+    signs, 1 / 3 / 8 groups, uneven load"""
     monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
     monkeypatch.setenv("HSFFT_BX_JITTER", jitter)
-    monkeypatch.setenv("HSFFT_BX_UL", "1")
     fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
     x = T.complex_input(n, 0xB8 ^ n ^ batch, batch=batch).reshape(batch, n)
     for sgn in (1, -1):

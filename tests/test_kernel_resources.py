@@ -40,8 +40,8 @@ BUDGETS = [
     (r"^_ZN2mr6k_row2ILi3ELi3ELi5ELi5ELi7ELi8ELi512ELb[01]ELb1ELb0ELi1ELb1ELb0ELi0EE", 0, 256, 2),
     # persistent Bluestein (c4): the whole grid (2 workgroups per CU) must be resident, so
     # 128 VGPRs is a hard limit; round 4's 8 dwords of spill went away in round 5 (the wait
-    # bound became a kernel argument: 127 VGPRs, no spill)
-    (r"^_ZN3bxc6k_bxcdILin?1ELb[01]EE", 0, 128, 4),
+    # bound became a kernel argument; 128 VGPRs with the unconditional P1 / P3 loads, no spill)
+    (r"^_ZN3bxc6k_bxcdILin?1EEE", 0, 128, 4),
 ]
 
 
