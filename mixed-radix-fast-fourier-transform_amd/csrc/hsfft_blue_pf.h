@@ -218,10 +218,7 @@ __global__ __launch_bounds__(512, 4) void k_bmid(Args a)
 /* Inverse FFT's second pass [8,8,8] at L = B = 512 (sign -S, conjugated twiddles) of q-tile
  * q0 for T rows, stored through the chirp for n < nsig (direction S).  Row prefetch (PREF)
  * is a template option the launcher does not use (as for pf::k_b512: with it the kernel spills 20 B). */
-/* UL (round 5, as bxc::k_bxcd's P3): the chirp values of four outputs loaded together at a
- * clamped index before their conditional stores, instead of each load inside its n < nsig
- * branch (hipcc waits vmcnt(0) after each: behind the previous element's store) */
-template <int T, int S, bool PREF = true, bool SPLIT = false, bool UL = false>
+template <int T, int S, bool PREF = true, bool SPLIT = false>
 __global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
 {
     constexpr int P = 512, TPG = 64, G = 8;
@@ -308,27 +305,10 @@ __global__ __launch_bounds__(512, SPLIT ? 6 : 4) void k_blast(Args a)
         /* output n = u*B + q, u = jt + 64 jj; only n < nsig is stored (ref :1871-1886) */
         double2 *orow = a.out + (long long)(b0 + it) * a.odist;
         const double2 *ch = a.saux;
-        if constexpr (UL) {
 #pragma unroll
-            for (int h4 = 0; h4 < 8; h4 += 4) {
-                double2 c4[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const unsigned n = (jt + (h4 + u) * TPG) * B + q;
-                    c4[u] = ch[n < nsig ? n : nsig - 1];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const unsigned n = (jt + (h4 + u) * TPG) * B + q;
-                    if (n < nsig) orow[n] = chirp_out<S>(xr[h4 + u], xi[h4 + u], c4[u]);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < 8; jj++) {
-                const unsigned n = (jt + jj * TPG) * B + q;
-                if (n < nsig) orow[n] = chirp_out<S>(xr[jj], xi[jj], ch[n]);
-            }
+        for (int jj = 0; jj < 8; jj++) {
+            const unsigned n = (jt + jj * TPG) * B + q;
+            if (n < nsig) orow[n] = chirp_out<S>(xr[jj], xi[jj], ch[n]);
         }
     }
 }
@@ -354,8 +334,6 @@ inline int launch(int which, const void *in, long long idist, void *out, long lo
     kfn fn;
     if (which == 2) fn = sgn == 1 ? k_bfirst<8, 1> : k_bfirst<8, -1>;
     else if (which == 0) fn = sgn == 1 ? k_bmid<8, 1> : k_bmid<8, -1>;
-    else if (env("HSFFT_BLAST_UL", 0)) /* round 5 A/B: the last kernel's chirp loads unconditional */
-        fn = sgn == 1 ? k_blast<8, 1, false, false, true> : k_blast<8, -1, false, false, true>;
     else fn = sgn == 1 ? k_blast<8, 1, false> : k_blast<8, -1, false>;
     Args a;
     memset(&a, 0, sizeof a);

@@ -163,26 +163,6 @@ def test_bluestein_row_looped_kernels(n, mask, xt, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("n,batch", [(99991, 5), (65537, 9), (131071, 17)])
-def test_bluestein_last_kernel_unconditional_chirp_loads(n, batch, monkeypatch):
-    """k_blast<..., UL = true> (HSFFT_BLAST_UL=1, round 5 A/B): the chirp values of four outputs
-    loaded together at a clamped index before their n < N stores -- bit-exact, both signs"""
-    monkeypatch.setenv("HSFFT_BLUE_XCD", "0")
-    monkeypatch.setenv("HSFFT_BLAST_UL", "1")
-    x = T.complex_input(n, 0xB9 ^ n, batch=batch).reshape(batch, n)
-    for sgn in (1, -1):
-        p = hsfft.Plan(n, sgn)
-        din = hsfft.DeviceBuffer.from_array(x)
-        dout = hsfft.DeviceBuffer(x.nbytes)
-        hsfft.exec_batched(p, din, dout, batch)
-        hsfft.synchronize()
-        y = dout.to_array(np.complex128).reshape(batch, n)
-        assert T.bits_equal(y, _oracle(x, sgn, ("blast_ul", n, batch))), (n, sgn)
-        din.free()
-        dout.free()
-        p.close()
-
-
 @pytest.mark.parametrize("ng,batch,jitter", [("8", 1, "0"), ("8", 5, "0"), ("8", 19, "0"), ("3", 7, "0"), ("1", 2, "0"),
                                              ("8", 19, "3"), ("3", 7, "5"), ("8", 19, "m0"), ("8", 19, "m0j3")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
