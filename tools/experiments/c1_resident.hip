@@ -6,6 +6,8 @@
 //   r2) the small fft_exec path's data movement: host memcpy of 16 KB into a page-locked slot,
 //       request; the kernel copies the 16 KB slot -> slot over the host link, fences, answers;
 //       host memcpy of the 16 KB result out -- compare with c1_latency's (f)
+//   r3) as r2 with every thread's four loads issued before its stores (r2's loop waits for each
+//       load, and -- vmcnt being in order -- for the previous element's store, before the next)
 // The kernel leaves on a stop word, or after 200 ms without a request (100 MHz counter), so a
 // host that dies cannot leave it running.  Host waits are bounded too.
 // Build: hipcc -O2 --offload-arch=gfx950 c1_resident.hip -o c1_resident (binary git-ignored)
@@ -57,6 +59,14 @@ __global__ __launch_bounds__(256) void k_service(unsigned *words, const double2 
             __atomic_thread_fence(__ATOMIC_ACQUIRE); /* every thread: the host's slot writes */
             for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = in[i];
             __syncthreads();
+        } else if (mode == 3) { /* n == 1024, 256 threads */
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            double2 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = in[threadIdx.x + 256 * k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) out[threadIdx.x + 256 * k] = v[k];
+            __syncthreads();
         }
         if (threadIdx.x == 0) {
             __threadfence_system();
@@ -89,7 +99,7 @@ static int run(int mode, unsigned *words, double2 *hin, double2 *hout, double &u
     for (int r = 1; r <= R + 100 && !rc; r++) {
         for (int i = 0; i < 1024; i++) user[i] = make_double2(r + i, -i);
         const auto t0 = clk::now();
-        if (mode == 2) memcpy(hin, user.data(), 16384);
+        if (mode >= 2) memcpy(hin, user.data(), 16384);
         __atomic_store_n(words, (unsigned)r, __ATOMIC_RELEASE);
         long spins = 0;
         while (__atomic_load_n(words + 16, __ATOMIC_ACQUIRE) != (unsigned)r)
@@ -98,9 +108,9 @@ static int run(int mode, unsigned *words, double2 *hin, double2 *hout, double &u
                 rc = 1;
                 break;
             }
-        if (mode == 2 && !rc) memcpy(back.data(), hout, 16384);
+        if (mode >= 2 && !rc) memcpy(back.data(), hout, 16384);
         const auto t1 = clk::now();
-        if (mode == 2 && !rc && (back[1023].x != r + 1023.0 || back[0].x != (double)r)) {
+        if (mode >= 2 && !rc && (back[1023].x != r + 1023.0 || back[0].x != (double)r)) {
             fprintf(stderr, "mode %d: wrong data at request %d\n", mode, r);
             rc = 1;
         }
@@ -121,11 +131,13 @@ int main()
     CK(hipHostMalloc((void **)&words, 256, hipHostMallocCoherent));
     CK(hipHostMalloc((void **)&hin, 16384, hipHostMallocCoherent));
     CK(hipHostMalloc((void **)&hout, 16384, hipHostMallocCoherent));
-    double r1 = 0, r2 = 0;
+    double r1 = 0, r2 = 0, r3 = 0;
     if (run(1, words, hin, hout, r1)) return 1;
     printf("resident ping-pong (no data): median %.2f us\n", r1);
     if (run(2, words, hin, hout, r2)) return 1;
     printf("resident 16 KB slot copy + host memcpy in / out: median %.2f us\n", r2);
+    if (run(3, words, hin, hout, r3)) return 1;
+    printf("resident 16 KB slot copy, loads issued together, + host memcpy in / out: median %.2f us\n", r3);
     CK(hipHostFree(words));
     CK(hipHostFree(hin));
     CK(hipHostFree(hout));
