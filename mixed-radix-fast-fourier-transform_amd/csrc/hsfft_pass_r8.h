@@ -280,8 +280,11 @@ constexpr int occ_hint()
     return FIRST && thr == 512 && w >= 6 ? 6 : 1;
 }
 
-template <int R0, int N8, int G, int WQ, bool FIRST, bool SPLIT, bool HOOK>
-__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (occ_hint<R0, N8, G, FIRST, SPLIT>())) void k_pass(Args a)
+/* TWA (round 5): every stage's twiddles loaded right behind the inputs instead of one stage at a
+ * time -- for the one-workgroup launches of the small host-buffer path (c1), whose input loads
+ * cross the host link, so the stages' dependent table loads no longer follow one another */
+template <int R0, int N8, int G, int WQ, bool FIRST, bool SPLIT, bool HOOK, bool TWA = false>
+__global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (TWA ? 1 : occ_hint<R0, N8, G, FIRST, SPLIT>())) void k_pass(Args a)
 {
     using S = Shape<R0, N8>;
     constexpr int P = S::P, TPG = S::TPG, WM = G / WQ;
@@ -331,7 +334,26 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (occ_hint<R0, N8, G, FIRS
     constexpr bool CTW = !FIRST && G == 8 && WQ == 8 && !SPLIT && P * G >= 8 * (TPG * G / 64) * 56;
     const long long q0 = q - g % WQ;
     double2 wa[7], wb[7];
-    if constexpr (FIRST) { /* tiny, cache-resident tables: load at use, keep VGPRs low */
+    if constexpr (FIRST && TWA) {
+        static_assert(N8 <= 3 && G == 1, "TWA: one-workgroup first passes up to 4096 points");
+        double2 w1[7], w2[7], w3[7];
+        if constexpr (N8 >= 1) load_tw<8, S::Lloc(1), TPG>(w1, a, jt, q, valid);
+        if constexpr (N8 >= 2) load_tw<8, S::Lloc(2), TPG>(w2, a, jt, q, valid);
+        if constexpr (N8 >= 3) load_tw<8, S::Lloc(3), TPG>(w3, a, jt, q, valid);
+        do_stage<R0, 1, TPG>(xr, xi, wa, a, jt, q, true);
+        if constexpr (N8 >= 1) {
+            exchange<R0, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            do_stage<8, S::Lloc(1), TPG>(xr, xi, w1, a, jt, q, false);
+        }
+        if constexpr (N8 >= 2) {
+            exchange<8, S::Lloc(1), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            do_stage<8, S::Lloc(2), TPG>(xr, xi, w2, a, jt, q, false);
+        }
+        if constexpr (N8 >= 3) {
+            exchange<8, S::Lloc(2), 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
+            do_stage<8, S::Lloc(3), TPG>(xr, xi, w3, a, jt, q, false);
+        }
+    } else if constexpr (FIRST) { /* tiny, cache-resident tables: load at use, keep VGPRs low */
         do_stage<R0, 1, TPG>(xr, xi, wa, a, jt, q, true);
         if constexpr (N8 >= 1) {
             exchange<R0, 1, 8, TPG, P, G, SPLIT>(xr, xi, lds, jt, g);
@@ -710,6 +732,13 @@ static const Variant k_variants[] = {
 };
 #undef R8V
 
+/* TWA first passes (G = 1, no hooks) for the small path's one-workgroup launches */
+#define R8T(r0, n8) {r0, n8, 1, 1, true, false, false, k_pass<r0, n8, 1, 1, true, false, false, true>}, \
+                    {r0, n8, 1, 1, true, true, false, k_pass<r0, n8, 1, 1, true, true, false, true>}
+static const Variant k_twa[] = {R8T(2, 3), R8T(4, 3), R8T(8, 3), R8T(2, 2), R8T(4, 2), R8T(8, 2),
+                                R8T(2, 1), R8T(4, 1), R8T(8, 1)};
+#undef R8T
+
 inline const Variant *find(int r0, int n8, int G, int WQ, bool first, bool split = false, bool hook = false)
 {
     for (const Variant &v : k_variants)
@@ -814,6 +843,12 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         a.done = l->done;
         a.done_val = l->done_val;
         *l->armed = 1;
+        /* HSFFT_SMALL_TWA (default 1): the one-workgroup first pass with every stage's twiddles
+         * loaded behind its inputs */
+        const char *te = getenv("HSFFT_SMALL_TWA");
+        if (first && !hook && p->G == 1 && !(te && atoi(te) == 0))
+            for (const Variant &t : k_twa)
+                if (t.r0 == v->r0 && t.n8 == v->n8 && t.split == v->split) v = &t;
     }
     const size_t lds = (size_t)p->P * p->G * (split ? sizeof(double) : sizeof(double2));
     if (grid <= 0 || grid > 0x7fffffffLL || threads > 1024 || lds > 160 * 1024) {
