@@ -335,7 +335,7 @@ __global__ __launch_bounds__((Shape<R0, N8>::TPG * G), (TWA ? 1 : occ_hint<R0, N
     const long long q0 = q - g % WQ;
     double2 wa[7], wb[7];
     if constexpr (FIRST && TWA) {
-        static_assert(N8 <= 3 && G == 1, "TWA: one-workgroup first passes up to 4096 points");
+        static_assert(N8 <= 3 && G == 1 && TPG <= 256, "TWA: one-workgroup first passes up to 2048 points");
         double2 w1[7], w2[7], w3[7];
         if constexpr (N8 >= 1) load_tw<8, S::Lloc(1), TPG>(w1, a, jt, q, valid);
         if constexpr (N8 >= 2) load_tw<8, S::Lloc(2), TPG>(w2, a, jt, q, valid);
@@ -735,8 +735,9 @@ static const Variant k_variants[] = {
 /* TWA first passes (G = 1, no hooks) for the small path's one-workgroup launches */
 #define R8T(r0, n8) {r0, n8, 1, 1, true, false, false, k_pass<r0, n8, 1, 1, true, false, false, true>}, \
                     {r0, n8, 1, 1, true, true, false, k_pass<r0, n8, 1, 1, true, true, false, true>}
-static const Variant k_twa[] = {R8T(2, 3), R8T(4, 3), R8T(8, 3), R8T(2, 2), R8T(4, 2), R8T(8, 2),
-                                R8T(2, 1), R8T(4, 1), R8T(8, 1)};
+/* up to 2048 points (256 threads): at 4096 (512 threads, 150 VGPRs) measured slower, 23.28 vs
+ * 22.86 us per fft_exec (profiles/r05l_c1_twa.txt) */
+static const Variant k_twa[] = {R8T(2, 3), R8T(4, 3), R8T(2, 2), R8T(4, 2), R8T(8, 2), R8T(2, 1), R8T(4, 1), R8T(8, 1)};
 #undef R8T
 
 inline const Variant *find(int r0, int n8, int G, int WQ, bool first, bool split = false, bool hook = false)
