@@ -22,6 +22,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 #include "hsfft_butterfly.h"
 #include "hsfft_internal.h"
@@ -916,21 +917,69 @@ int hsd_cu_count(void)
     return n;
 }
 
+/* objects of exited threads, released by a live thread (hsd_reap) */
+namespace {
+enum GraveKind { G_STREAM, G_EVENT, G_DEV, G_HOST };
+struct Grave {
+    GraveKind kind;
+    int dev;
+    void *p;
+};
+std::mutex g_grave_mtx;
+std::vector<Grave> g_grave;
+std::atomic<int> g_grave_n{0};
+
+void bury(GraveKind kind, int dev, void *p)
+{
+    if (!p) return;
+    std::lock_guard<std::mutex> g(g_grave_mtx);
+    g_grave.push_back(Grave{kind, dev, p});
+    g_grave_n.store((int)g_grave.size(), std::memory_order_release);
+}
+}  // namespace
+
 void hsd_thread_release(void)
 {
     for (int d = 0; d < HS_MAX_DEV; d++) {
-        if (t_own[d]) {
-            (void)hipStreamSynchronize(t_own[d]);
-            (void)hipStreamDestroy(t_own[d]);
-            t_own[d] = 0;
-        }
-        if (t_spin_have[d]) {
-            (void)hipEventDestroy(t_spin_ev[d]);
-            t_spin_have[d] = false;
-        }
-        pl_release_thread(d);
+        bury(G_STREAM, d, (void *)t_own[d]);
+        t_own[d] = 0;
+        if (t_spin_have[d]) bury(G_EVENT, d, (void *)t_spin_ev[d]);
+        t_spin_have[d] = false;
+        bury(G_DEV, d, t_pl[d].dev);
+        bury(G_HOST, d, t_pl[d].host);
+        t_pl[d].dev = nullptr;
+        t_pl[d].host = nullptr;
     }
+}
+
+void hsd_host_free_deferred(void *p) { bury(G_HOST, -1, p); }
+
+int hsd_reap(void)
+{
+    if (g_grave_n.load(std::memory_order_acquire) == 0) return 0;
+    std::vector<Grave> list;
+    {
+        std::lock_guard<std::mutex> g(g_grave_mtx);
+        list.swap(g_grave);
+        g_grave_n.store(0, std::memory_order_release);
+    }
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    for (const Grave &o : list) {
+        if (o.dev >= 0) (void)hipSetDevice(o.dev);
+        switch (o.kind) {
+        case G_STREAM: /* the exited thread's last work may still run */
+            (void)hipStreamSynchronize((hipStream_t)o.p);
+            (void)hipStreamDestroy((hipStream_t)o.p);
+            break;
+        case G_EVENT: (void)hipEventDestroy((hipEvent_t)o.p); break;
+        case G_DEV: (void)hipFree(o.p); break;
+        case G_HOST: (void)hipHostFree(o.p); break;
+        }
+    }
+    if (cur >= 0) (void)hipSetDevice(cur);
     (void)hipGetLastError();
+    return (int)list.size();
 }
 
 /* Releases every device object this layer holds on the current device (after waiting for its

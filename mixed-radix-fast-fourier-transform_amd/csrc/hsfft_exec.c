@@ -550,6 +550,7 @@ int hsfft_release_scratch(void)
     const int d = hs_lock_device();
     int rc = 0;
     if (hs_require_gpu() == 0) {
+        (void)hsd_reap(); /* and what exited threads left */
         rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
         for (int c = 0; c < HS_NSCRATCH; c++) {
             if (hsd_free(g_scr[d][c]) && !rc) rc = HSFFT_ERR_DEVICE;
@@ -561,7 +562,6 @@ int hsfft_release_scratch(void)
     return rc;
 }
 
-static void thread_resources_free(void *unused);
 void hs_crash_trace_install(void);
 static void *g_pin[HS_MAX_DEV][2];
 static size_t g_pin_sz[HS_MAX_DEV];
@@ -573,6 +573,7 @@ static size_t g_pin_sz[HS_MAX_DEV];
  * and error words, the calling thread's own slots / words / streams, the timing and ordering
  * events and the library streams.  Everything is re-created on demand.  Callers must not run
  * other library calls concurrently. */
+static void thread_pins_free_now(void);
 int hsfft_finalize(void)
 {
     g_errbuf[0] = 0;
@@ -580,7 +581,8 @@ int hsfft_finalize(void)
     if (rc) return rc;
     const int cur = hsd_get_device();
     hs_conv_cache_release(); /* frees plans: their device state on every device goes with them */
-    thread_resources_free(NULL);
+    thread_pins_free_now();  /* its streams, events and error words: hsd_finalize_device below */
+    (void)hsd_reap();        /* what exited threads left */
     const int ndev = hsd_device_count() < HS_MAX_DEV ? hsd_device_count() : HS_MAX_DEV;
     for (int d = 0; d < ndev; d++) {
         if (hsd_set_device(d)) {
@@ -1204,9 +1206,27 @@ static __thread unsigned t_seq;
 static pthread_key_t g_tkey;
 static pthread_once_t g_tkey_once = PTHREAD_ONCE_INIT;
 
+/* at thread exit: the thread's objects go to the device layer's list of leftovers, released
+ * by the next live call that reaps it (a new thread's first small call, hsfft_release_scratch,
+ * hsfft_finalize) -- a thread-exit destructor makes no HIP call (round 5: under rocprofv3 one
+ * that did aborted the process, the profiler's per-thread state being gone by then) */
 static void thread_resources_free(void *unused)
 {
     (void)unused;
+    for (int d = 0; d < HS_MAX_DEV; d++) {
+        hsd_host_free_deferred(t_pin[d][0]);
+        hsd_host_free_deferred(t_pin[d][1]);
+        hsd_host_free_deferred(t_flag[d]);
+        t_pin[d][0] = t_pin[d][1] = NULL;
+        t_pin_sz[d] = 0;
+        t_flag[d] = NULL;
+    }
+    hsd_thread_release();
+}
+
+/* hsfft_finalize: the calling (live) thread's page-locked slots and words, at once */
+static void thread_pins_free_now(void)
+{
     for (int d = 0; d < HS_MAX_DEV; d++) {
         hsd_host_free(t_pin[d][0]);
         hsd_host_free(t_pin[d][1]);
@@ -1215,7 +1235,6 @@ static void thread_resources_free(void *unused)
         t_pin_sz[d] = 0;
         t_flag[d] = NULL;
     }
-    hsd_thread_release();
 }
 
 static void tkey_init(void) { pthread_key_create(&g_tkey, thread_resources_free); }
@@ -1223,7 +1242,10 @@ static void tkey_init(void) { pthread_key_create(&g_tkey, thread_resources_free)
 static void thread_resources_used(void)
 {
     pthread_once(&g_tkey_once, tkey_init);
-    if (!pthread_getspecific(g_tkey)) pthread_setspecific(g_tkey, (void *)1);
+    if (!pthread_getspecific(g_tkey)) {
+        pthread_setspecific(g_tkey, (void *)1);
+        (void)hsd_reap(); /* a new thread: release what exited ones left */
+    }
 }
 
 static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *oup)

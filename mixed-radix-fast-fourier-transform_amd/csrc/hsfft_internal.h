@@ -102,9 +102,14 @@ int hsd_host_register(void *p, size_t bytes);
 int hsd_host_unregister(void *p);
 void *hsd_host_alloc(size_t bytes);  /* page-locked, device-accessible host memory */
 int hsd_host_free(void *p);
-/* release the calling thread's own device objects (its per-device streams, polling events);
- * called from the thread-exit destructor of the host side */
+/* Thread-exit side (round 5): hand the calling thread's own device objects (its per-device
+ * streams, polling events, persistent-launch error words) -- and, hsd_host_free_deferred, its
+ * page-locked blocks -- to a list that a live thread releases with hsd_reap().  Called from the
+ * host side's thread-exit destructor, which must not call HIP: by then the runtime's (and a
+ * profiler's) own per-thread state may be gone (rocprofv3 aborted the process there). */
 void hsd_thread_release(void);
+void hsd_host_free_deferred(void *p);
+int hsd_reap(void); /* release what exited threads left (any thread; returns the objects freed) */
 int hsd_event_record(int i);      /* event ring (64 slots) on the selected stream */
 int hsd_event_wait(int i);
 void *hsd_stream(void);

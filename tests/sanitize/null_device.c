@@ -10,6 +10,7 @@
  */
 #include <stdint.h>
 #include <stdio.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
@@ -117,6 +118,30 @@ void *hsd_stream(void) { return NULL; }
  * destructor ran once per thread that used the concurrent small path */
 int null_thread_releases;
 void hsd_thread_release(void) { __atomic_fetch_add(&null_thread_releases, 1, __ATOMIC_RELAXED); }
+/* page-locked blocks of exited threads: kept on a list until a live thread reaps it (so ASan
+ * sees a leak if nothing ever does, and a use-after-free if a block is freed too early) */
+static pthread_mutex_t null_grave_mtx = PTHREAD_MUTEX_INITIALIZER;
+static void *null_grave[256];
+static int null_grave_n;
+int null_reaped;
+void hsd_host_free_deferred(void *p)
+{
+    if (!p) return;
+    pthread_mutex_lock(&null_grave_mtx);
+    if (null_grave_n < 256) null_grave[null_grave_n++] = p;
+    else free(p);
+    pthread_mutex_unlock(&null_grave_mtx);
+}
+int hsd_reap(void)
+{
+    pthread_mutex_lock(&null_grave_mtx);
+    const int n = null_grave_n;
+    for (int i = 0; i < n; i++) free(null_grave[i]);
+    null_grave_n = 0;
+    pthread_mutex_unlock(&null_grave_mtx);
+    __atomic_fetch_add(&null_reaped, n, __ATOMIC_RELAXED);
+    return n;
+}
 /* "device" memory is host memory here: pointers the tests pass as device buffers are
  * malloc'd, so every pointer counts as a device pointer -- except the buffers a test marks
  * as host buffers (null_mark_host), which take the host-pointer paths of fft_exec (the

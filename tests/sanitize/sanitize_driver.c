@@ -323,6 +323,17 @@ int main(void)
         free_fft(g_small);
         const int rel = __atomic_load_n(&null_thread_releases, __ATOMIC_RELAXED) - rel0;
         CHECK(rel == 4, "per-thread resources released at thread exit: %d of 4 threads", rel);
+        /* their page-locked slots wait for a live thread: the next new thread's first small
+         * call reaps them (the exit destructor itself makes no device call) */
+        extern int null_reaped;
+        const int reaped0 = __atomic_load_n(&null_reaped, __ATOMIC_RELAXED);
+        g_small = fft_init(1024, 1);
+        pthread_t lt;
+        pthread_create(&lt, NULL, small_caller, (void *)0L);
+        pthread_join(lt, NULL);
+        free_fft(g_small);
+        const int reaped = __atomic_load_n(&null_reaped, __ATOMIC_RELAXED) - reaped0;
+        CHECK(reaped >= 8, "slots of exited threads reaped by a new thread: %d (4 threads x 2 slots + words)", reaped);
     }
 
     g_shared = fft_init(12600, 1);
