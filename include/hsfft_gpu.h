@@ -133,7 +133,11 @@ long long hsfft_bluestein_fallbacks(void);
  * distinct plans (the reference's mixed-radix fft_exec is reentrant, highSpeedFFT.c:1920).
  * Calls that run on the same device are serialised per call by a device lock (they share
  * the device's stream and scratch pool); calls on different devices run concurrently.
- * Freeing a plan while another thread still executes it remains a caller error. */
+ * Freeing a plan while another thread still executes it remains a caller error.
+ * A thread's own objects (the small host-buffer path's page-locked slots and stream, its
+ * Bluestein error words) outlive it briefly: they are released by the next call that starts on
+ * a new thread, by hsfft_release_scratch() or by hsfft_finalize() -- never from the exiting
+ * thread itself, where the HIP runtime's per-thread state may already be gone. */
 
 /* --- multi-device (single process; one host thread per device, no collective) --------- */
 /* Shards the batch contiguously over devices 0..ndev-1: h-side arrays of per-device
