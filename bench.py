@@ -111,6 +111,25 @@ def row_range(rank, per_rank_batch):
     return rank * per_rank_batch, (rank + 1) * per_rank_batch
 
 
+def rank_fields(comm, ws, wall_s, steps, ev_ms_per_step, bytes_per_step):
+    """Per-rank breakdown of the timed region: every rank's
+    own wall ms per step (between the same barriers), its event-timed ms per step and the
+    algorithmic bytes it moved / its event time against ONE GPU's peak, plus the aggregate --
+    the bytes of all ranks / the max-over-ranks wall time -- against ws x the peak.  Collective
+    calls: every rank must call this."""
+    walls = comm.gather(wall_s / steps * 1e3)
+    evs = comm.gather(ev_ms_per_step)
+    per = []
+    for r in range(ws):
+        ach = bytes_per_step / (evs[r] / 1e3) / 1e9 if evs[r] > 0 else 0.0
+        per.append({"rank": r, "ms_per_step": round(walls[r], 4), "event_ms_per_step": round(evs[r], 4),
+                    "achieved": round(ach, 3), "frac": round(ach / HBM_PEAK_GBS, 6)})
+    agg = bytes_per_step * ws / (max(walls) / 1e3) / 1e9 if max(walls) > 0 else 0.0
+    return per, {"achieved": round(agg, 3), "peak": HBM_PEAK_GBS * ws, "unit": "GB/s",
+                 "frac": round(agg / (HBM_PEAK_GBS * ws), 6),
+                 "basis": f"algorithmic bytes of all {ws} ranks / the max-over-ranks wall ms per step"}
+
+
 def dry_run(args, comm, ws, rank):
     """The multi-rank control path without a GPU (CPU tests under gloo): every rank transforms
     its own rows of a small c2c batch with the CPU oracle, timed with the same barrier /
@@ -133,17 +152,24 @@ def dry_run(args, comm, ws, rank):
     for _ in range(args.steps):
         run()
     comm.barrier()
-    wall = comm.max(time.perf_counter() - t0)
+    local = time.perf_counter() - t0
+    wall = comm.max(local)
     rows = comm.gather(r0)
     checks = comm.gather(float(np.abs(y).sum()))
     lib.orc_plan_destroy(p)
     ms = wall / args.steps * 1e3
+    # the same per-rank / aggregate fields as a GPU line (the CPU "event" time is the wall time)
+    per, agg = rank_fields(comm, ws, local, args.steps, local / args.steps * 1e3, n * batch * 32)
     if rank == 0:
-        print(json.dumps({"metric": f"dry run: c2c N={n} on the CPU oracle (no GPU)", "value": round(
+        out = {"metric": f"dry run: c2c N={n} on the CPU oracle (no GPU)", "value": round(
             n * batch * ws / (ms / 1e3) / 1e9, 6), "unit": "GSamples/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "dry_run": True, "per_rank_batch": batch, "row_starts": [int(r) for r in rows],
-            "rank_checksums": checks}), flush=True)
+            "rank_checksums": checks, "per_rank": per,
+            "roofline": {"bound": "hbm", "unit": "GB/s", "aggregate": agg}}
+        if not args.no_cpu_baseline:  # rank 0, after the timed region, as on the GPU line
+            out["cpu_baseline"] = cpu_baseline(("c2c", n, batch, 0x5EED0002, ""), seconds_target=0.5)
+        print(json.dumps(out), flush=True)
 
 
 def host_cores():
@@ -568,6 +594,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch (development only)")
     ap.add_argument("--n", type=int, default=0, help="override the transform length (development only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="wall-time target of the cpu_baseline leg's timed sweeps (tests shorten it)")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="c2, one rank: skip timing BASELINE configs c1, c3, c4, c5 after the headline")
     ap.add_argument("--r2c-compact", action="store_true",
@@ -703,7 +731,8 @@ def bench_main(args, comm, ws, rank, local):
             run()
         hsfft.synchronize()
         comm.barrier()
-        return comm.max(time.perf_counter() - t0)
+        local = time.perf_counter() - t0
+        return comm.max(local), local
 
     # the buffers as first allocated -- what a caller's plain hipMalloc gets; no placement
     # selection (probe_placement only reports the output buffer's slice copy rates)
@@ -711,7 +740,7 @@ def bench_main(args, comm, ws, rank, local):
         place = probe_placement(din, dout)
         fill()
         hsfft.synchronize()
-    wall = timed_steps()
+    wall, wall_local = timed_steps()
 
     # HIP-event timing on the library stream (what the kernels take) + per-pass breakdown
     npass = 0
@@ -724,7 +753,8 @@ def bench_main(args, comm, ws, rank, local):
         ev_ms = wall * 1e3
     else:
         ev_ms = hsfft.time_r2c_batched(plan, din, dout, chunk, max(1, args.steps)) * (batch / chunk)
-    ev_step_ms = comm.max(ev_ms / max(1, args.steps))
+    ev_local_ms = ev_ms / max(1, args.steps)
+    ev_step_ms = comm.max(ev_local_ms)
 
     ms_per_step = wall / args.steps * 1e3
     value = samples * ws / (ms_per_step / 1e3) / 1e9
@@ -765,6 +795,9 @@ def bench_main(args, comm, ws, rank, local):
                        "basis": f"whole step: {bytes_per_sample} B x N x batch / event-timed step time, "
                                 f"{launches} of the step",
                        "kernel": kern or f"{launches} per step"}
+    if ws > 1:  # every rank's own numbers, and the whole job's bytes against ws x the peak
+        out["per_rank"], out["roofline"]["aggregate"] = rank_fields(comm, ws, wall_local, args.steps, ev_local_ms,
+                                                                    samples * bytes_per_sample)
     if pass_ms:
         out["roofline"]["pass_ms"] = [round(p, 4) for p in pass_ms]
         out["roofline"]["pass_frac"] = [round(samples * bytes_per_sample / (p / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
@@ -801,8 +834,10 @@ def bench_main(args, comm, ws, rank, local):
                                 "pcie_gbs": round(2 * hx.nbytes / hs / 1e9, 1),
                                 "note": "host (pageable numpy) rows in and out, upload/transform/download overlapped; "
                                         "PCIe-inclusive, not the headline value"}
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.c2r:
-        out["cpu_baseline"] = cpu_baseline(cfg)
+    if rank == 0 and not args.no_cpu_baseline and not args.c2r:
+        # rank 0, after every rank's timed region (at N > 1 too: north_star wants the reference
+        # timed on the host cores in the same run next to the 1/2/4/8-GPU numbers)
+        out["cpu_baseline"] = cpu_baseline(cfg, seconds_target=args.cpu_seconds)
     if ws == 1 and args.config == "c2" and not args.batch and not args.n and not args.no_other_configs:
         din.free()
         dout.free()

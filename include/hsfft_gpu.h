@@ -134,10 +134,16 @@ long long hsfft_bluestein_fallbacks(void);
  * Calls that run on the same device are serialised per call by a device lock (they share
  * the device's stream and scratch pool); calls on different devices run concurrently.
  * Freeing a plan while another thread still executes it remains a caller error.
- * A thread's own objects (the small host-buffer path's page-locked slots and stream, its
- * Bluestein error words) outlive it briefly: they are released by the next call that starts on
- * a new thread, by hsfft_release_scratch() or by hsfft_finalize() -- never from the exiting
- * thread itself, where the HIP runtime's per-thread state may already be gone. */
+ * A thread's own objects (the small host-buffer path's page-locked slots, completion word and
+ * stream, its Bluestein error words) are recycled when it exits: they are parked per device and
+ * the next thread to use that device takes them over (an exited thread's pending Bluestein error
+ * is discarded, never passed on).  Nothing is created or destroyed on the exiting thread, where
+ * the HIP runtime's per-thread state may already be gone, nor on a new thread's path; the parked
+ * sets are destroyed by hsfft_release_scratch() and hsfft_finalize(). */
+
+/* Per-thread streams created by the process so far (diagnostics: with threads recycled through
+ * the pool, at most the number of threads that ever used the library AT ONCE, per device). */
+long long hsfft_thread_streams_created(void);
 
 /* --- multi-device (single process; one host thread per device, no collective) --------- */
 /* Shards the batch contiguously over devices 0..ndev-1: h-side arrays of per-device

@@ -39,8 +39,19 @@
  *
  * Residency: every workgroup of a group waits on the others, so the whole grid must be
  * resident.  The host checks the occupancy API and refuses a grid that does not fit (its rows
- * run on the three-launch path).  If something else occupies the GPU the waits time out, the
- * kernel exits and sets the error word: a synchronous call re-runs the rows through the
+ * run on the three-launch path).  The kernel then PROVES residency with an arrival census
+ * (round 6): a group's hand-offs only ever wait on the same group, so every workgroup counts
+ * itself into its GROUP's census counter and waits until all 64 tiles of the group have
+ * arrived before its first hand-off wait.  The census gives up only when no new member has
+ * arrived for `climit` ticks.  Synchronous calls (which re-run a failed launch's rows on the
+ * three-launch path themselves) use ~2 ms: a group the occupancy API over-promised
+ * (MI355X_MICROARCH.md: the API can report one block per CU too many at some SGPR counts) then
+ * fails in ~2 ms instead of after the ~1.3 s hand-off bound.  Asynchronous calls, which cannot
+ * re-run, keep the ~1.3 s bound, so a group waiting for slots that a complete group (or a short
+ * kernel of another stream) will free is delayed, not failed.  A group whose 64 members are all
+ * resident never waits in the census beyond their dispatch, and once its census is complete no
+ * hand-off wait of that group can be a residency deadlock.  A failed census or a timed-out wait
+ * sets the error word and the kernel exits: a synchronous call re-runs the rows through the
  * three-launch path (hsfft_exec.c run_bluestein), an asynchronous one reports the error at the
  * caller's next hsfft_synchronize().
  *
@@ -57,6 +68,7 @@
 namespace bxc {
 
 constexpr unsigned long long T_LIMIT = 1ull << 27; /* bounded waits: ~1.3 s of the 100 MHz real-time counter */
+constexpr unsigned long long C_LIMIT = 200000;   /* census of a synchronous call: ~2 ms without a new arrival */
 
 constexpr unsigned NTILE = 64;  /* 8-column tiles of the 512 x 512 image = workgroups per group */
 constexpr unsigned CS = 32;     /* counter stride (128-B line per counter) */
@@ -72,12 +84,12 @@ struct XArgs {
     const double2 *hk;    /* M transformed chirp values */
     double2 *img;         /* [ng][NIMG][IMG] */
     long long idist, odist;
-    unsigned *cnt;        /* [ng][2] counters, CS apart */
+    unsigned *cnt;        /* [ng][2] hand-off counters, then [ng] census counters, each on its own line (CS apart) */
     unsigned *err;        /* sticky error word (set on a timed-out wait; every wait gives up once it is set) */
     unsigned long long tlimit; /* wait bound in ticks of the 100 MHz real-time counter (T_LIMIT; tests lower it) */
+    unsigned long long climit; /* census bound: ticks without a new arrival (C_LIMIT sync, T_LIMIT async) */
     unsigned batch, ng, nsig, sleep;
     unsigned jitter;      /* > 0: pseudo-random per-phase delays (uneven-load tests; results unchanged) */
-    unsigned merge;       /* 1: one acquire per iteration when both counters are already complete */
     unsigned xmap;        /* 1: a group spans the XCDs (XCD x owns tiles [8x, 8x+8) of every group) */
     unsigned *dbg;        /* optional per-workgroup trace (8 words): rows, P1, wait A, P2, wait B, P3 */
 };
@@ -125,12 +137,11 @@ __device__ __forceinline__ void arrive(const XArgs &a, unsigned *c, unsigned k, 
 
 /* wait until the group's counter c reaches `target` (R1 consumer: one lane polls relaxed, then
  * ONE agent-scope acquire and its vmcnt(0), then the barrier every wave joins before loading);
- * false on timeout (~1.3 s without progress of this one wait) or sticky error.  If c2 is given
- * and has already reached target2 when c is satisfied, the same acquire covers it too and
- * *both is set (the caller then skips its wait on c2: one acquire per iteration instead of
- * two). */
+ * false on timeout (~1.3 s without progress of this one wait) or sticky error.  (Round 4's
+ * merged form -- one acquire per iteration when both counters were already complete -- measured
+ * +3.9 % slower and was removed in round 6.) */
 __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned target, unsigned *sflag, unsigned k,
-                                      unsigned ph, unsigned *c2 = nullptr, unsigned target2 = 0, bool *both = nullptr)
+                                      unsigned ph)
 {
     if (threadIdx.x == 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); /* deadline per wait */
@@ -144,16 +155,47 @@ __device__ __forceinline__ bool await(const XArgs &a, unsigned *c, unsigned targ
                 break;
             }
         }
-        if (!st && c2 && __hip_atomic_load(c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target2) st = 2;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); /* buffer_inv sc1: drop this CU's stale L1 lines */
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the invalidate has completed */
         *sflag = st;
     }
     jitter_sleep(a, k, ph + 8);
     __syncthreads();
-    const unsigned st = __builtin_amdgcn_readfirstlane(*sflag);
-    if (both) *both = st == 2;
-    return (st & 1) == 0;
+    return __builtin_amdgcn_readfirstlane(*sflag) == 0;
+}
+
+/* Arrival census of one group: thread 0 counts the workgroup in, then polls the group's census
+ * until all `n` members have arrived; false (error word bit 4 set) when no member arrived for
+ * climit ticks, or when the error word is set (a workgroup gave up, possibly before this one was
+ * dispatched).  Relaxed atomics: the census orders no data (the hand-offs acquire their own). */
+__device__ __forceinline__ bool census(const XArgs &a, unsigned *cs, unsigned n, unsigned *sflag)
+{
+    if (threadIdx.x == 0) {
+        unsigned st = 0;
+        unsigned seen = __hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (seen < n) {
+            for (unsigned n = 0; n < a.sleep; n++) __builtin_amdgcn_s_sleep(2);
+            if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                st = 1;
+                break;
+            }
+            const unsigned now = __hip_atomic_load(cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (now != seen) { /* progress: the bound restarts */
+                seen = now;
+                t0 = t;
+            } else if (t - t0 > a.climit) {
+                __hip_atomic_fetch_or(a.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                st = 1;
+                break;
+            }
+        }
+        if (!st && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) st = 1;
+        *sflag = st;
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(*sflag) == 0;
 }
 
 /* Round 5: every load of P1 (input row, chirp) and P3 (chirp) is issued unconditionally at a
@@ -207,6 +249,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
     double2 *imgs = a.img + (size_t)grp * NIMG * IMG; /* image 1 [2], image 2 [2] */
     unsigned *cA = a.cnt + (size_t)grp * 2 * CS, *cB = cA + CS;
     const unsigned R = grp < a.batch ? (a.batch - grp + ng - 1) / ng : 0; /* this group's rows */
+    if (R && !census(a, a.cnt + (size_t)(2 * ng + grp) * CS, NTILE, sflag)) return;
     unsigned tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}; /* debug: rows, P1, wait A, P2, wait B, P3, P1 / P2 store drain (10 ns) */
 
     /* skewed pipeline: iteration k runs P3 of row k-2, P2 of row k-1, P1 of row k, so every
@@ -230,10 +273,8 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
     }
         double xr[8], xi[8];
         double2 w[7];
-        bool a_ready = false; /* A(k) observed complete before P3's acquire: P2 needs no wait */
         if (k >= 2) { /* ---- P3 of row k-2: k_blast's body on image 2 [k&1], chirp store */
-            if (!await(a, cB, (k - 1) * NTILE, sflag, k, 0, a.merge && k <= R ? cA : nullptr, k * NTILE, &a_ready))
-                return;
+            if (!await(a, cB, (k - 1) * NTILE, sflag, k, 0)) return;
             BX_MARK(4)
             /* per-thread indices from an opaque copy of threadIdx in every phase, so the
              * compiler does not hoist all three phases' addresses out of the loop (spills) */
@@ -286,7 +327,7 @@ __global__ __launch_bounds__(512, 4) void k_bxcd(XArgs a)
             tr[0]++;
         }
         if (k >= 1 && k <= R) { /* ---- P2 of row k-1: k_bmid's body, image 1 -> image 2 [(k-1)&1] */
-            if (!a_ready && !await(a, cA, k * NTILE, sflag, k, 1)) return;
+            if (!await(a, cA, k * NTILE, sflag, k, 1)) return;
             BX_MARK(2)
             unsigned tt = tid;
             asm volatile("" : "+v"(tt));

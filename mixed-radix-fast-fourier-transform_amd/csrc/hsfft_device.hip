@@ -66,6 +66,7 @@ hipStream_t g_stream2[HS_MAX_DEV], g_stream3[HS_MAX_DEV];
 std::atomic<bool> g_stream2_init[HS_MAX_DEV], g_stream3_init[HS_MAX_DEV];
 thread_local int t_sidx = 0; /* 0: library stream, 1: pipeline / H2D stream, 2: D2H stream, 3: this thread's own */
 thread_local hipStream_t t_own[HS_MAX_DEV]; /* per-thread streams (concurrent small fft_exec calls) */
+std::atomic<long long> g_own_created{0};       /* per-thread streams created (diagnostics) */
 
 int cur_dev()
 {
@@ -83,7 +84,10 @@ hipStream_t stream()
     if (t_sidx == 0) return primary();
     const int dev = cur_dev();
     if (t_sidx == 3) {
-        if (!t_own[dev] && hipStreamCreateWithFlags(&t_own[dev], hipStreamNonBlocking) != hipSuccess) t_own[dev] = 0;
+        if (!t_own[dev]) { /* (a thread adopts an exited thread's stream first: hsd_thread_adopt) */
+            if (hipStreamCreateWithFlags(&t_own[dev], hipStreamNonBlocking) != hipSuccess) t_own[dev] = 0;
+            else g_own_created.fetch_add(1, std::memory_order_relaxed);
+        }
         return t_own[dev];
     }
     if (t_sidx == 2) return lazy_stream(g_stream3, g_stream3_init, dev);
@@ -655,16 +659,28 @@ static size_t g_pl_bytes[HS_MAX_DEV];
  * cleared only by hsd_sync_report() of the thread that launched (hsfft_synchronize, the timing
  * calls), so no other synchronisation -- a scratch pool growing, a device state being built, an
  * unrelated plan's call, another thread -- can consume or inherit it.  The synchronous word is
- * cleared before every synchronous launch and read right after it (hsd_blue_xcd returns 2). */
+ * cleared before every synchronous launch and read right after it (hsd_blue_xcd returns 2).
+ * Words adopted from an exited thread (hsd_thread_adopt) are `inherited`: whatever that thread's
+ * asynchronous launches left in word 0 is discarded, never reported to the new owner -- on the
+ * library stream, behind those launches, before the new owner's first launch (pl_words), or at
+ * the new owner's first report (pl_report, after the stream was waited for). */
 struct PlErr {
     unsigned *dev;  /* 64 words on the device: [0] async sticky, [32] sync */
     unsigned *host; /* 64 page-locked words: copies of the same */
+    bool inherited;
 };
 static thread_local PlErr t_pl[HS_MAX_DEV];
 
 static int pl_words(int dev, PlErr **out)
 {
     PlErr *p = &t_pl[dev];
+    if (p->dev && p->inherited) {
+        /* the exited owner's asynchronous launches ran on the library stream: clear word 0 and
+         * its host copy behind them */
+        HCHK(hipMemsetAsync(p->dev, 0, sizeof(unsigned), primary()));
+        HCHK(hipMemcpyAsync(p->host, p->dev, sizeof(unsigned), hipMemcpyDeviceToHost, primary()));
+        p->inherited = false;
+    }
     if (!p->dev) {
         HCHK(hipMalloc((void **)&p->dev, 64 * sizeof(unsigned)));
         if (hipMemset(p->dev, 0, 64 * sizeof(unsigned)) != hipSuccess ||
@@ -687,6 +703,7 @@ static void pl_release_thread(int dev)
     if (p->host) (void)hipHostFree(p->host);
     p->dev = nullptr;
     p->host = nullptr;
+    p->inherited = false;
 }
 
 /* Report (once) a timed-out wait of this thread's asynchronous persistent launches on the
@@ -697,11 +714,18 @@ static int pl_report(void)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) return 0;
     PlErr *p = &t_pl[dev];
-    if (!p->host || *(volatile unsigned *)p->host == 0) return 0;
+    if (!p->host || *(volatile unsigned *)p->host == 0) {
+        p->inherited = false; /* (an inherited word 0 was clear: nothing to discard) */
+        return 0;
+    }
     const unsigned w = *(volatile unsigned *)p->host;
     *(volatile unsigned *)p->host = 0;
     (void)hipMemsetAsync(p->dev, 0, sizeof(unsigned), primary());
     (void)hipStreamSynchronize(primary());
+    if (p->inherited) { /* the exited owner's error: discarded, not this thread's */
+        p->inherited = false;
+        return 0;
+    }
     snprintf(g_err, sizeof g_err,
              "persistent Bluestein launch: an in-launch dependency wait timed out (error word %u); the outputs of this "
              "thread's Bluestein calls since its last hsfft_synchronize() on this device are invalid "
@@ -723,35 +747,13 @@ int hsd_sync_report(void)
     return pl_report();
 }
 
-/* wait for the library stream by polling an event (no blocking wait / wake-up): for short
- * synchronous calls (the small host-buffer fft_exec) */
-static thread_local hipEvent_t t_spin_ev[HS_MAX_DEV];
-static thread_local bool t_spin_have[HS_MAX_DEV];
-
-int hsd_sync_spin(void)
-{
-    hipEvent_t *ev = t_spin_ev;
-    bool *have = t_spin_have;
-    const int dev = cur_dev();
-    if (!have[dev]) {
-        HCHK(hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming));
-        have[dev] = true;
-    }
-    HCHK(hipEventRecord(ev[dev], primary()));
-    for (;;) {
-        const hipError_t e = hipEventQuery(ev[dev]);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) return set_err(e, "hipEventQuery");
-    }
-    return 0;
-}
-
 /* Bluestein M = 2^18 as one persistent launch (hsfft_blue_xcd.h).  img: ng x 4 x M points of
  * scratch.  Every workgroup must be resident at once: the occupancy API is asked on the host
  * and a grid that does not fit is refused (returned as 3: the caller runs the three-launch
- * path at once).  HSFFT_BX_COOP=1 launches through hipLaunchCooperativeKernel instead, which
- * makes the runtime do the same check (round 4's default; DESIGN.md §5 round 5 for why it is
- * not the default any more).
+ * path at once); inside the launch a per-group arrival census proves it (a synchronous call's
+ * grid the API over-promised fails in ~2 ms, as a timed-out launch).  (Round 4's hipLaunchCooperativeKernel form crashed
+ * profiled processes at exit; removed in round 6.)  HSFFT_BX_UNCHECKED=1
+ * (tests only) skips the host check, so that the census has to catch an oversized grid.
  * Asynchronous (sync == 0): the launch is queued on the library stream with a copy of this
  * thread's sticky error word behind it; a wait that still timed out (the last-resort bound,
  * ~1.3 s without progress; HSFFT_BX_TLIMIT ticks of the 100 MHz counter for tests) is reported
@@ -771,9 +773,8 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     void (*fn)(bxc::XArgs) = sgn == 1 ? bxc::k_bxcd<1> : bxc::k_bxcd<-1>;
     HCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bxc::LDS_BYTES));
     const int grid = ng * (int)bxc::NTILE;
-    const char *ce = getenv("HSFFT_BX_COOP");
-    const bool coop = ce && atoi(ce);
-    if (!coop) { /* co-residency: workgroups per CU the occupancy API allows x CUs */
+    const char *ue = getenv("HSFFT_BX_UNCHECKED");
+    if (!(ue && atoi(ue))) { /* co-residency: workgroups per CU the occupancy API allows x CUs */
         int per_cu = 0, ncu = 0;
         HCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, 512, bxc::LDS_BYTES));
         HCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -789,7 +790,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         if (rc) return rc;
     }
     const size_t CS = bxc::CS;
-    const size_t need = 2 * CS * (size_t)ng * sizeof(unsigned);
+    const size_t need = 3 * CS * (size_t)ng * sizeof(unsigned); /* hand-off counters + census per group */
     if (g_pl_bytes[dev] < need) {
         if (g_pl_ctr[dev]) {
             HCHK(hipStreamSynchronize(stream())); /* an earlier launch may still use the block */
@@ -822,6 +823,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     a.ng = (unsigned)ng;
     a.nsig = (unsigned)nsig;
     a.tlimit = bxc::T_LIMIT;
+    a.climit = sync ? bxc::C_LIMIT : bxc::T_LIMIT; /* fail fast only where the caller re-runs the rows */
     {
         /* polls of the hand-off counters 4 x s_sleep 2 apart (was 1): in-process A/B on two boxes
          * 32.51 vs 32.61 and 32.13 vs 32.29 ms per 8192 rows (profiles/r05e_*, r05g_*) */
@@ -831,12 +833,10 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         a.xmap = e ? (unsigned)atoi(e) & 1u : 1u;
         e = getenv("HSFFT_BX_JITTER"); /* uneven-load tests: per-phase delays, results unchanged */
         a.jitter = e ? (unsigned)atoi(e) : 0u;
-        /* HSFFT_BX_MERGE=1: one acquire per iteration where both counters are already done --
-         * measured slower (c4 23.6-23.7 vs 24.3-24.5 GSamples/s with one acquire per wait) */
-        e = getenv("HSFFT_BX_MERGE");
-        a.merge = e ? (unsigned)atoi(e) & 1u : 0u;
         e = getenv("HSFFT_BX_TLIMIT"); /* tests: force the timeout path (ticks of 10 ns) */
         if (e && atoll(e) > 0) a.tlimit = (unsigned long long)atoll(e);
+        e = getenv("HSFFT_BX_CLIMIT"); /* tests: the census bound (ticks of 10 ns) */
+        if (e && atoll(e) > 0) a.climit = (unsigned long long)atoll(e);
     }
     static unsigned *s_dbg[HS_MAX_DEV];
     const char *dbgenv = getenv("HSFFT_BX_DEBUG");
@@ -847,23 +847,8 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
         a.dbg = s_dbg[dev];
         sync = 1;
     }
-    if (coop) {
-        void *kargs[] = {&a};
-        const hipError_t le = hipLaunchCooperativeKernel((const void *)fn, dim3((unsigned)grid), dim3(512), kargs,
-                                                         (unsigned)bxc::LDS_BYTES, stream());
-        if (le != hipSuccess) {
-            (void)hipGetLastError();
-            if (le == hipErrorCooperativeLaunchTooLarge) {
-                snprintf(g_err, sizeof g_err, "hsd_blue_xcd: cooperative launch of %d workgroups refused (not co-resident)",
-                         grid);
-                return 3; /* refused at launch: the caller runs the three-launch path */
-            }
-            return set_err(le, "hipLaunchCooperativeKernel(k_bxcd)");
-        }
-    } else {
-        hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
-        HCHK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
+    HCHK(hipGetLastError());
     /* host copy of the word this launch could set (async: the cumulative sticky word) */
     unsigned *hw = sync ? pe->host + 32 : pe->host;
     HCHK(hipMemcpyAsync(hw, err, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
@@ -917,69 +902,80 @@ int hsd_cu_count(void)
     return n;
 }
 
-/* objects of exited threads, released by a live thread (hsd_reap) */
+/* Pool of per-thread sets (hsfft_internal.h, hsd_tset): parked by exiting threads, adopted by
+ * new ones, destroyed only by hsd_pool_drain.  Parking and adopting are host bookkeeping under a
+ * mutex -- no HIP call (round 5's reaping synchronised and freed dead threads' objects on a new
+ * thread's first call: +52 % per threaded small call). */
 namespace {
-enum GraveKind { G_STREAM, G_EVENT, G_DEV, G_HOST };
-struct Grave {
-    GraveKind kind;
-    int dev;
-    void *p;
+struct TSet {
+    hipStream_t own;
+    PlErr pl;
+    hsd_tset h;
 };
-std::mutex g_grave_mtx;
-std::vector<Grave> g_grave;
-std::atomic<int> g_grave_n{0};
-
-void bury(GraveKind kind, int dev, void *p)
-{
-    if (!p) return;
-    std::lock_guard<std::mutex> g(g_grave_mtx);
-    g_grave.push_back(Grave{kind, dev, p});
-    g_grave_n.store((int)g_grave.size(), std::memory_order_release);
-}
+std::mutex g_pool_mtx;
+std::vector<TSet> g_pool[HS_MAX_DEV];
 }  // namespace
 
-void hsd_thread_release(void)
+long long hsd_thread_streams_created(void) { return g_own_created.load(std::memory_order_relaxed); }
+
+void hsd_thread_park(int dev, const hsd_tset *h)
 {
-    for (int d = 0; d < HS_MAX_DEV; d++) {
-        bury(G_STREAM, d, (void *)t_own[d]);
-        t_own[d] = 0;
-        if (t_spin_have[d]) bury(G_EVENT, d, (void *)t_spin_ev[d]);
-        t_spin_have[d] = false;
-        bury(G_DEV, d, t_pl[d].dev);
-        bury(G_HOST, d, t_pl[d].host);
-        t_pl[d].dev = nullptr;
-        t_pl[d].host = nullptr;
-    }
+    if (dev < 0 || dev >= HS_MAX_DEV) return;
+    TSet s;
+    s.own = t_own[dev];
+    s.pl = t_pl[dev];
+    s.h = h ? *h : hsd_tset{{nullptr, nullptr}, 0, nullptr};
+    t_own[dev] = 0;
+    t_pl[dev] = PlErr{nullptr, nullptr, false};
+    if (!s.own && !s.pl.dev && !s.h.pin[0] && !s.h.pin[1] && !s.h.flag) return;
+    std::lock_guard<std::mutex> g(g_pool_mtx);
+    g_pool[dev].push_back(s);
 }
 
-void hsd_host_free_deferred(void *p) { bury(G_HOST, -1, p); }
-
-int hsd_reap(void)
+int hsd_thread_adopt(int dev, hsd_tset *h)
 {
-    if (g_grave_n.load(std::memory_order_acquire) == 0) return 0;
-    std::vector<Grave> list;
+    if (dev < 0 || dev >= HS_MAX_DEV || t_own[dev] || t_pl[dev].dev) return 0;
+    TSet s;
     {
-        std::lock_guard<std::mutex> g(g_grave_mtx);
-        list.swap(g_grave);
-        g_grave_n.store(0, std::memory_order_release);
+        std::lock_guard<std::mutex> g(g_pool_mtx);
+        if (g_pool[dev].empty()) return 0;
+        s = g_pool[dev].back();
+        g_pool[dev].pop_back();
     }
-    int cur = -1;
+    t_own[dev] = s.own; /* the stream's earlier work was waited for by its call */
+    t_pl[dev] = s.pl;
+    t_pl[dev].inherited = s.pl.dev != nullptr;
+    if (h) *h = s.h;
+    return 1;
+}
+
+int hsd_pool_drain(void)
+{
+    std::vector<TSet> sets[HS_MAX_DEV];
+    {
+        std::lock_guard<std::mutex> g(g_pool_mtx);
+        for (int d = 0; d < HS_MAX_DEV; d++) sets[d].swap(g_pool[d]);
+    }
+    int cur = -1, n = 0;
     (void)hipGetDevice(&cur);
-    for (const Grave &o : list) {
-        if (o.dev >= 0) (void)hipSetDevice(o.dev);
-        switch (o.kind) {
-        case G_STREAM: /* the exited thread's last work may still run */
-            (void)hipStreamSynchronize((hipStream_t)o.p);
-            (void)hipStreamDestroy((hipStream_t)o.p);
-            break;
-        case G_EVENT: (void)hipEventDestroy((hipEvent_t)o.p); break;
-        case G_DEV: (void)hipFree(o.p); break;
-        case G_HOST: (void)hipHostFree(o.p); break;
+    for (int d = 0; d < HS_MAX_DEV; d++) {
+        if (sets[d].empty()) continue;
+        (void)hipSetDevice(d);
+        for (const TSet &s : sets[d]) { /* the stream first: its work may use the rest */
+            if (s.own) {
+                (void)hipStreamSynchronize(s.own);
+                (void)hipStreamDestroy(s.own);
+            }
+            if (s.pl.dev) (void)hipFree(s.pl.dev);
+            if (s.pl.host) (void)hipHostFree(s.pl.host);
+            for (void *p : {s.h.pin[0], s.h.pin[1], (void *)s.h.flag})
+                if (p) (void)hipHostFree(p);
+            n++;
         }
     }
     if (cur >= 0) (void)hipSetDevice(cur);
     (void)hipGetLastError();
-    return (int)list.size();
+    return n;
 }
 
 /* Releases every device object this layer holds on the current device (after waiting for its
@@ -1003,10 +999,6 @@ int hsd_finalize_device(void)
         (void)hipStreamSynchronize(t_own[dev]);
         (void)hipStreamDestroy(t_own[dev]);
         t_own[dev] = 0;
-    }
-    if (t_spin_have[dev]) {
-        (void)hipEventDestroy(t_spin_ev[dev]);
-        t_spin_have[dev] = false;
     }
     std::lock_guard<std::mutex> g(g_init_mtx);
     if (g_pl_ctr[dev]) (void)hipFree(g_pl_ctr[dev]);

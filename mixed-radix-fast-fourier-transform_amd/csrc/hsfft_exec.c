@@ -550,7 +550,7 @@ int hsfft_release_scratch(void)
     const int d = hs_lock_device();
     int rc = 0;
     if (hs_require_gpu() == 0) {
-        (void)hsd_reap(); /* and what exited threads left */
+        (void)hsd_pool_drain(); /* and the parked per-thread sets of exited threads */
         rc = hsd_sync() ? HSFFT_ERR_DEVICE : 0;
         for (int c = 0; c < HS_NSCRATCH; c++) {
             if (hsd_free(g_scr[d][c]) && !rc) rc = HSFFT_ERR_DEVICE;
@@ -582,7 +582,7 @@ int hsfft_finalize(void)
     const int cur = hsd_get_device();
     hs_conv_cache_release(); /* frees plans: their device state on every device goes with them */
     thread_pins_free_now();  /* its streams, events and error words: hsd_finalize_device below */
-    (void)hsd_reap();        /* what exited threads left */
+    (void)hsd_pool_drain();  /* the parked per-thread sets of exited threads */
     const int ndev = hsd_device_count() < HS_MAX_DEV ? hsd_device_count() : HS_MAX_DEV;
     for (int d = 0; d < ndev; d++) {
         if (hsd_set_device(d)) {
@@ -832,16 +832,6 @@ static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long
     l.store_op = store_op;
     l.store_aux = saux;
     l.nsig = nsig;
-    /* HSFFT_NT bit0/1: first pass nt load/store, bit2/3: last pass nt load/store */
-    const int nt = env_int("HSFFT_NT", 0);
-    if (i == 0) {
-        l.nt_load = nt & 1;
-        l.nt_store = (nt >> 1) & 1;
-    }
-    if (i == e->npass - 1) {
-        l.nt_load |= (nt >> 2) & 1;
-        l.nt_store |= (nt >> 3) & 1;
-    }
 #ifdef HSFFT_DEV_PROBES
     /* development build only: every row aliased to one buffer (on-die timing, results wrong) */
     if (env_int("HSFFT_DEV_ALIAS", 0) & 1) l.idist = l.odist = 0;
@@ -851,7 +841,9 @@ static int launch_pass(hs_entry *e, hs_devstate *ds, int i, const void *in, long
     return rc;
 }
 
-/* Two-pass chain over the batch in chunks of `chunk` rows, software-pipelined over two
+#ifdef HSFFT_DEV_PROBES
+/* Development build only (round 6: measured slower, 52-67 vs 91 GSamples/s on c2 -- DESIGN.md
+ * §5).  Two-pass chain over the batch in chunks of `chunk` rows, software-pipelined over two
  * streams: pass A of chunk k+1 (library stream) overlaps pass B of chunk k (second stream),
  * ordered by events; at most `lag` chunks run ahead so the in-flight intermediates stay in
  * the 256 MiB Infinity Cache.  The library stream waits for the last pass B at the end. */
@@ -879,6 +871,7 @@ static int run_pipelined(hs_entry *e, hs_devstate *ds, const void *I, long long 
     if (!rc && k > 0) rc = hsd_event_wait(2 * (k - 1) + 1);
     return rc;
 }
+#endif
 
 /* One mixed-radix transform of length M per row, chained over the plan's passes.  Reads
  * I (never written), writes O.  Intermediate buffers come from the scratch pool; the last
@@ -907,12 +900,14 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
         long long per = (long long)(chunk_bytes() / (sizeof(fft_data) * (size_t)M));
         if (per < 1) per = 1;
         if (chunk > per) chunk = per;
-    } else {
-        /* optional: run all passes over a few rows at a time so the intermediate stays in
-         * the 256 MiB Infinity Cache between passes (HSFFT_MALL_ROWS) */
+    }
+#ifdef HSFFT_DEV_PROBES
+    else { /* development build only: all passes over a few rows at a time, the intermediate in
+            * the 256 MiB Infinity Cache between passes (HSFFT_MALL_ROWS; measured slower) */
         const int rows = env_int("HSFFT_MALL_ROWS", 0);
         if (rows > 0 && chunk > rows) chunk = rows;
     }
+#endif
     void *S[2] = {NULL, NULL};
     for (int k = 0; k < need; k++) {
         S[k] = hs_scratch(k, sizeof(fft_data) * (size_t)(chunk * M));
@@ -921,10 +916,10 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
             return HSFFT_ERR_NOMEM;
         }
     }
+#ifdef HSFFT_DEV_PROBES
     if (!need && n == 2 && chunk < batch && env_int("HSFFT_PIPE", 0))
         return run_pipelined(e, ds, I, idist, O, odist, batch, (int)chunk, sgn, conj, dir, load_op, laux, store_op,
                              saux, nsig);
-#ifdef HSFFT_DEV_PROBES
     const int dev_np = env_int("HSFFT_DEV_NPASS", 0); /* development build only: stop after this many passes */
 #else
     const int dev_np = 0;
@@ -957,9 +952,10 @@ static int run_chain(hs_entry *e, hs_devstate *ds, const void *I, long long idis
 
 /* persistent Bluestein launches whose rows ran on the three-launch path instead (grid not
  * co-resident, or waits timed out in a synchronous call); hsfft_bluestein_fallbacks() */
-static void thread_resources_used(void);
+static void thread_resources_used(int d);
 static long long g_blue_fallbacks;
 
+long long hsfft_thread_streams_created(void) { return hsd_thread_streams_created(); }
 long long hsfft_bluestein_fallbacks(void) { return __atomic_load_n(&g_blue_fallbacks, __ATOMIC_RELAXED); }
 
 /* Bluestein (ref :1735-1907) on rows of length N: pre-multiply fused into the first pass of
@@ -990,7 +986,7 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
     const int sync = t_sync_call > 0 || env_int("HSFFT_BX_SYNC", 0);
     long long done = 0;
     if (fuse && ng > 0) {
-        thread_resources_used(); /* this thread's error words are freed when it exits */
+        thread_resources_used(hsd_get_device()); /* this thread's error words are recycled when it exits */
         const size_t ib = (size_t)ng * 4 * sizeof(fft_data) * (size_t)M; /* 4 images per group */
         void *img = hs_scratch(3, ib);
         int rc = img ? 0 : 1;
@@ -1144,7 +1140,7 @@ static int small_host_exec(hs_entry *e, const fft_data *inp, fft_data *oup, size
     }
     memcpy(g_pin[d][0], inp, bytes);
     int rc = hs_c2c_rows(e, g_pin[d][0], e->N, g_pin[d][1], e->N, 1);
-    if (!rc) rc = env_int("HSFFT_SMALL_SPIN", 0) ? hsd_sync_spin() : hsd_sync();
+    if (!rc) rc = hsd_sync();
     if (!rc) memcpy(oup, g_pin[d][1], bytes);
     return rc;
 }
@@ -1200,28 +1196,28 @@ static __thread size_t t_pin_sz[HS_MAX_DEV];
 static __thread unsigned *t_flag[HS_MAX_DEV];
 static __thread unsigned t_seq;
 
-/* Per-thread resources (page-locked slots, completion words, the thread's own streams) are
- * released when the thread exits: a pthread key whose destructor runs in the exiting thread,
- * so callers that recycle or spawn threads do not leak pinned memory or streams. */
+/* Per-thread resources (page-locked slots, completion words, the thread's own streams and
+ * persistent-launch error words) are recycled, not destroyed, when the thread exits: a pthread
+ * key whose destructor runs in the exiting thread parks them in the device layer's pool
+ * (hsd_thread_park, no HIP call -- round 5: under rocprofv3 a HIP call there aborted the
+ * process), and a thread's first use of a device adopts a parked set (hsd_thread_adopt).  So a
+ * caller that recycles or spawns threads neither leaks pinned memory or streams nor pays for
+ * creating and destroying them; hsfft_release_scratch / hsfft_finalize destroy the pool. */
 static pthread_key_t g_tkey;
 static pthread_once_t g_tkey_once = PTHREAD_ONCE_INIT;
+static __thread unsigned t_adopted; /* bit d: this thread has taken its set of device d */
 
-/* at thread exit: the thread's objects go to the device layer's list of leftovers, released
- * by the next live call that reaps it (a new thread's first small call, hsfft_release_scratch,
- * hsfft_finalize) -- a thread-exit destructor makes no HIP call (round 5: under rocprofv3 one
- * that did aborted the process, the profiler's per-thread state being gone by then) */
 static void thread_resources_free(void *unused)
 {
     (void)unused;
     for (int d = 0; d < HS_MAX_DEV; d++) {
-        hsd_host_free_deferred(t_pin[d][0]);
-        hsd_host_free_deferred(t_pin[d][1]);
-        hsd_host_free_deferred(t_flag[d]);
+        const hsd_tset h = {{t_pin[d][0], t_pin[d][1]}, t_pin_sz[d], t_flag[d]};
+        hsd_thread_park(d, &h);
         t_pin[d][0] = t_pin[d][1] = NULL;
         t_pin_sz[d] = 0;
         t_flag[d] = NULL;
     }
-    hsd_thread_release();
+    t_adopted = 0;
 }
 
 /* hsfft_finalize: the calling (live) thread's page-locked slots and words, at once */
@@ -1235,16 +1231,25 @@ static void thread_pins_free_now(void)
         t_pin_sz[d] = 0;
         t_flag[d] = NULL;
     }
+    t_adopted = 0; /* a later first use may adopt a parked set again */
 }
 
 static void tkey_init(void) { pthread_key_create(&g_tkey, thread_resources_free); }
 
-static void thread_resources_used(void)
+/* this thread is about to use its own resources on device d: arm the exit destructor, and on
+ * the thread's first use of d take a set an exited thread parked (if any) */
+static void thread_resources_used(int d)
 {
     pthread_once(&g_tkey_once, tkey_init);
-    if (!pthread_getspecific(g_tkey)) {
-        pthread_setspecific(g_tkey, (void *)1);
-        (void)hsd_reap(); /* a new thread: release what exited ones left */
+    if (!pthread_getspecific(g_tkey)) pthread_setspecific(g_tkey, (void *)1);
+    if (d < 0 || d >= HS_MAX_DEV || (t_adopted >> d & 1u)) return;
+    t_adopted |= 1u << d;
+    hsd_tset h;
+    if (!t_pin[d][0] && !t_pin[d][1] && !t_flag[d] && hsd_thread_adopt(d, &h)) {
+        t_pin[d][0] = h.pin[0];
+        t_pin[d][1] = h.pin[1];
+        t_pin_sz[d] = h.pin_sz;
+        t_flag[d] = h.flag;
     }
 }
 
@@ -1272,7 +1277,7 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
         hs_entry_put(e);
         return 1;
     }
-    thread_resources_used();
+    thread_resources_used(d);
     if (t_pin_sz[d] < bytes) {
         hsd_host_free(t_pin[d][0]);
         hsd_host_free(t_pin[d][1]);

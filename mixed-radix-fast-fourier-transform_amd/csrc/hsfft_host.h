@@ -14,8 +14,9 @@ extern "C" {
 
 /* per-device state of one plan: device copies of what the plan needs */
 typedef struct hs_devstate {
-    void *d_tw;   /* M-1 (+1) complex twiddles, copied from the public struct; mixed-radix plans
-                   * with M <= 65536 also hold the last stage's block transposed at d_tw + M */
+    void *d_tw;   /* M-1 (+1) complex twiddles, copied from the public struct; only the
+                   * [3,3,5,5,7,8] whole-row schedule (N = 12600) also holds the last stage's block
+                   * transposed at d_tw + M, and readers are told so by tw_t below */
     void *d_gcs;  /* odd-radix cos/sin constants */
     void *d_chirp;/* Bluestein chirp h(n), N complex */
     void *d_hk;   /* Bluestein spectrum of the scaled, mirrored chirp, M complex */

@@ -62,7 +62,6 @@ typedef struct {
     int load_op, store_op;
     const void *load_aux, *store_aux;
     long long nsig;
-    int nt_load, nt_store;          /* non-temporal input / output (register kernels) */
     int tw_t;                       /* 1: tw + M holds the last stage's block transposed ([i-1][k]) */
     /* completion word (small host-buffer calls): a kernel that runs as ONE workgroup stores
      * done_val into *done (page-locked host memory) after every wave published its output at
@@ -84,7 +83,6 @@ int hsd_d2d_async(void *d, const void *s, size_t bytes);
 int hsd_memset_async(void *d, int v, size_t bytes);
 int hsd_sync(void);               /* wait for the library stream (a pending launch error stays pending) */
 int hsd_sync_report(void);        /* the same, then report this thread's pending persistent-launch error */
-int hsd_sync_spin(void);          /* hsd_sync polling an event instead of a blocking wait */
 /* release every device object of the device layer on the current device (streams, events,
  * persistent-launch counters, this thread's error words); re-created on demand */
 int hsd_finalize_device(void);
@@ -102,14 +100,24 @@ int hsd_host_register(void *p, size_t bytes);
 int hsd_host_unregister(void *p);
 void *hsd_host_alloc(size_t bytes);  /* page-locked, device-accessible host memory */
 int hsd_host_free(void *p);
-/* Thread-exit side (round 5): hand the calling thread's own device objects (its per-device
- * streams, polling events, persistent-launch error words) -- and, hsd_host_free_deferred, its
- * page-locked blocks -- to a list that a live thread releases with hsd_reap().  Called from the
- * host side's thread-exit destructor, which must not call HIP: by then the runtime's (and a
- * profiler's) own per-thread state may be gone (rocprofv3 aborted the process there). */
-void hsd_thread_release(void);
-void hsd_host_free_deferred(void *p);
-int hsd_reap(void); /* release what exited threads left (any thread; returns the objects freed) */
+/* Per-thread resources of one device, recycled (round 6).  A thread's own stream and
+ * persistent-launch error words (device layer) and its page-locked staging slots and completion
+ * word (host side, `hsd_tset`) form one set per device.  At thread exit the set is PARKED in the
+ * device's pool -- no HIP call: the exit destructor runs when the runtime's (and a profiler's)
+ * per-thread state may be gone (round 5: rocprofv3 aborted the process there).  A thread's first
+ * use of a device ADOPTS a parked set, again without a HIP call, so threads that come and go
+ * (thread pools, hsfft_exec_multi's shard threads) reuse streams and pinned memory instead of
+ * creating and destroying them on a live caller's path.  Sets are destroyed only by
+ * hsd_pool_drain (hsfft_release_scratch, hsfft_finalize). */
+typedef struct {
+    void *pin[2];     /* page-locked in / out slots of the small path (hsd_host_alloc) */
+    size_t pin_sz;    /* bytes of each slot */
+    unsigned *flag;   /* page-locked completion word (hsd_host_alloc) */
+} hsd_tset;
+void hsd_thread_park(int dev, const hsd_tset *h); /* thread exit: this thread's set of `dev` */
+int hsd_thread_adopt(int dev, hsd_tset *h);       /* 1: a parked set was taken (host part in *h) */
+int hsd_pool_drain(void); /* destroy every parked set, every device (streams waited first); returns the count */
+long long hsd_thread_streams_created(void); /* per-thread streams created so far (diagnostics) */
 int hsd_event_record(int i);      /* event ring (64 slots) on the selected stream */
 int hsd_event_wait(int i);
 void *hsd_stream(void);

@@ -68,6 +68,7 @@ SIGNATURES = {
     "hsfft_exec_multi": (CI, [VP, VP, VP, CI, CI]),
     "hsfft_bench_copy": (CI, [VP, VP, ctypes.c_size_t, CI, ctypes.POINTER(ctypes.c_float)]),
     "hsfft_bluestein_fallbacks": (ctypes.c_longlong, []),
+    "hsfft_thread_streams_created": (ctypes.c_longlong, []),
     "hsfft_count_diff_words": (CI, [VP, VP, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]),
 }
 

@@ -76,10 +76,12 @@ int hsd_sync_report(void)
     snprintf(err, sizeof err, "null device: persistent launch timed out");
     return -2;
 }
-int hsd_sync_spin(void) { return 0; }
 int null_finalized;
+static __thread void *own_tok[16]; /* this thread's own stream per device (hsd_thread_park) */
 int hsd_finalize_device(void)
 {
+    free(own_tok[cur_dev]); /* the calling thread's own stream */
+    own_tok[cur_dev] = NULL;
     __atomic_fetch_add(&null_finalized, 1, __ATOMIC_RELAXED);
     return hsd_sync_report();
 }
@@ -105,7 +107,12 @@ int hsd_stream_signal_wait(unsigned *flag, unsigned v)
 }
 int hsd_host_register(void *p, size_t bytes) { return 0; }
 int hsd_host_unregister(void *p) { return 0; }
-void *hsd_host_alloc(size_t bytes) { return malloc(bytes ? bytes : 16); }
+int null_host_allocs; /* page-locked blocks allocated (counted by the driver) */
+void *hsd_host_alloc(size_t bytes)
+{
+    __atomic_fetch_add(&null_host_allocs, 1, __ATOMIC_RELAXED);
+    return malloc(bytes ? bytes : 16);
+}
 int hsd_host_free(void *p)
 {
     free(p);
@@ -114,32 +121,78 @@ int hsd_host_free(void *p)
 int hsd_event_record(int i) { return i < 0 ? -1 : 0; }
 int hsd_event_wait(int i) { return i < 0 ? -1 : 0; }
 void *hsd_stream(void) { return NULL; }
-/* per-thread objects released at thread exit: counted, so the driver can check the
- * destructor ran once per thread that used the concurrent small path */
-int null_thread_releases;
-void hsd_thread_release(void) { __atomic_fetch_add(&null_thread_releases, 1, __ATOMIC_RELAXED); }
-/* page-locked blocks of exited threads: kept on a list until a live thread reaps it (so ASan
- * sees a leak if nothing ever does, and a use-after-free if a block is freed too early) */
-static pthread_mutex_t null_grave_mtx = PTHREAD_MUTEX_INITIALIZER;
-static void *null_grave[256];
-static int null_grave_n;
-int null_reaped;
-void hsd_host_free_deferred(void *p)
+/* per-thread sets (hsd_tset + the thread's own stream, modelled as a heap token created on
+ * the thread's first launch on its own stream): parked at thread exit, adopted by a new thread's
+ * first use of the device, freed by hsd_pool_drain -- so ASan reports a set that is lost (leak)
+ * or freed while still in use, and the driver counts the streams and page-locked blocks
+ * created (they must stay at the number of threads alive at once) */
+#define NULL_POOL 256
+typedef struct {
+    void *tok;
+    hsd_tset h;
+} null_set;
+static pthread_mutex_t null_pool_mtx = PTHREAD_MUTEX_INITIALIZER;
+static null_set null_pool[16][NULL_POOL];
+static int null_pool_n[16];
+int null_parks, null_adopts, null_drained;
+long long null_streams_created;
+static void own_stream_used(void)
 {
-    if (!p) return;
-    pthread_mutex_lock(&null_grave_mtx);
-    if (null_grave_n < 256) null_grave[null_grave_n++] = p;
-    else free(p);
-    pthread_mutex_unlock(&null_grave_mtx);
+    if (sidx == 3 && !own_tok[cur_dev]) {
+        own_tok[cur_dev] = malloc(1);
+        __atomic_fetch_add(&null_streams_created, 1, __ATOMIC_RELAXED);
+    }
 }
-int hsd_reap(void)
+long long hsd_thread_streams_created(void) { return __atomic_load_n(&null_streams_created, __ATOMIC_RELAXED); }
+void hsd_thread_park(int dev, const hsd_tset *h)
 {
-    pthread_mutex_lock(&null_grave_mtx);
-    const int n = null_grave_n;
-    for (int i = 0; i < n; i++) free(null_grave[i]);
-    null_grave_n = 0;
-    pthread_mutex_unlock(&null_grave_mtx);
-    __atomic_fetch_add(&null_reaped, n, __ATOMIC_RELAXED);
+    if (dev < 0 || dev >= 16) return;
+    null_set s = {own_tok[dev], {{NULL, NULL}, 0, NULL}};
+    if (h) s.h = *h;
+    own_tok[dev] = NULL;
+    if (!s.tok && !s.h.pin[0] && !s.h.pin[1] && !s.h.flag) return;
+    pthread_mutex_lock(&null_pool_mtx);
+    if (null_pool_n[dev] < NULL_POOL) null_pool[dev][null_pool_n[dev]++] = s;
+    else { /* (never in the driver: it would show as a lower adopt count) */
+        free(s.tok);
+        free(s.h.pin[0]);
+        free(s.h.pin[1]);
+        free(s.h.flag);
+    }
+    pthread_mutex_unlock(&null_pool_mtx);
+    __atomic_fetch_add(&null_parks, 1, __ATOMIC_RELAXED);
+}
+int hsd_thread_adopt(int dev, hsd_tset *h)
+{
+    if (dev < 0 || dev >= 16 || own_tok[dev]) return 0;
+    pthread_mutex_lock(&null_pool_mtx);
+    const int have = null_pool_n[dev] > 0;
+    null_set s = {NULL, {{NULL, NULL}, 0, NULL}};
+    if (have) s = null_pool[dev][--null_pool_n[dev]];
+    pthread_mutex_unlock(&null_pool_mtx);
+    if (!have) return 0;
+    own_tok[dev] = s.tok;
+    if (h) *h = s.h;
+    __atomic_fetch_add(&null_adopts, 1, __ATOMIC_RELAXED);
+    return 1;
+}
+int hsd_pool_drain(void)
+{
+    int n = 0;
+    pthread_mutex_lock(&null_pool_mtx);
+    for (int d = 0; d < 16; d++) {
+        for (int i = 0; i < null_pool_n[d]; i++) {
+            null_set *s = &null_pool[d][i];
+            free(s->tok);
+            free(s->h.pin[0]);
+            free(s->h.pin[1]);
+            free(s->h.flag);
+            n++;
+        }
+        null_pool_n[d] = 0;
+    }
+    pthread_mutex_unlock(&null_pool_mtx);
+    __atomic_fetch_add(&null_drained, n, __ATOMIC_RELAXED);
     return n;
 }
 /* "device" memory is host memory here: pointers the tests pass as device buffers are
@@ -206,7 +259,10 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     /* a launch on a thread's own stream (the concurrent small fft_exec path) "runs" a little
      * later, as a queued kernel would: the window in which another thread could free what it
      * reads (tests the device-state pinning) */
-    if (sidx == 3) usleep(20);
+    if (sidx == 3) {
+        own_stream_used();
+        usleep(20);
+    }
     const long long M = (long long)p->P * p->A * p->B;
     const long long in_len = l->load_op == HS_LOAD_CHIRP ? l->nsig : M;
     const long long out_len = l->store_op == HS_STORE_CHIRP ? l->nsig : M;

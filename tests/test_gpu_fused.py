@@ -164,18 +164,16 @@ def test_bluestein_row_looped_kernels(n, mask, xt, monkeypatch):
 
 
 @pytest.mark.parametrize("ng,batch,jitter", [("8", 1, "0"), ("8", 5, "0"), ("8", 19, "0"), ("3", 7, "0"), ("1", 2, "0"),
-                                             ("8", 19, "3"), ("3", 7, "5"), ("8", 19, "m0"), ("8", 19, "m0j3")])
+                                             ("8", 19, "3"), ("3", 7, "5")])
 @pytest.mark.parametrize("n", [99991, 65537, 131071])
 def test_bluestein_persistent_launch(n, ng, batch, jitter, monkeypatch):
     """Bluestein M = 2^18 as one persistent launch (csrc/hsfft_blue_xcd.h: groups of 64
     workgroups carry a row through the three passes, intermediates handed over in-launch):
     fewer rows than groups, ragged last round, both signs, and under uneven load (HSFFT_BX_JITTER:
     pseudo-random per-phase delays scramble the hand-off order) -- bit-exact vs the oracle and
-    vs the three-launch path; no launch fell back.  m0: one acquire per wait instead of the
-    merged acquire per iteration (HSFFT_BX_MERGE=0)."""
+    vs the three-launch path; no launch fell back."""
     monkeypatch.setenv("HSFFT_BLUE_XCD", ng)
-    monkeypatch.setenv("HSFFT_BX_MERGE", "0" if jitter.startswith("m0") else "1")
-    monkeypatch.setenv("HSFFT_BX_JITTER", jitter[3:] if jitter.startswith("m0j") else ("0" if jitter == "m0" else jitter))
+    monkeypatch.setenv("HSFFT_BX_JITTER", jitter)
     fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
     x = T.complex_input(n, 0xB7 ^ n ^ batch, batch=batch).reshape(batch, n)
     for sgn in (1, -1):
@@ -223,21 +221,32 @@ def test_bluestein_persistent_unconditional_loads(n, ng, batch, jitter, monkeypa
     assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
 
 
-@pytest.mark.parametrize("mode", ["refused", "refused_coop", "sync"])
+@pytest.mark.parametrize("mode", ["refused", "sync", "census_sync", "unchecked_async"])
 def test_bluestein_persistent_launch_contract(mode, monkeypatch):
-    """The persistent Bluestein launch needs every workgroup resident at once.  refused: 9
-    groups = 576 workgroups of which only 512 (two per CU) can be resident, so the host's
-    occupancy check refuses the grid (refused_coop: HSFFT_BX_COOP=1, the runtime's cooperative
-    launch refuses it) and the rows run on the three-launch path at once -- results bit-exact,
-    one fallback counted per call, no ~1 s wait.  sync: HSFFT_BX_SYNC=1 (the synchronous form
-    with the automatic re-run) -- bit-exact, no fallback."""
+    """The persistent Bluestein launch needs every workgroup of a group resident at once.
+    refused: 9 groups = 576 workgroups of which only 512 (two per CU) can be resident, so the
+    host's occupancy check refuses the grid and the rows run on the three-launch path at once --
+    results bit-exact, one fallback counted per call, no ~1 s wait.  sync: HSFFT_BX_SYNC=1 (the
+    synchronous form with the automatic re-run) -- bit-exact, no fallback.
+    Round 6, the in-kernel arrival census, with the host check skipped
+    (HSFFT_BX_UNCHECKED=1) so the oversized grid is really launched:
+      census_sync: the 9 groups' workgroups interleaved (HSFFT_BX_MAP=0: group = block % 9), so
+        every group is partly resident and none can finish; the synchronous call's census gives
+        up after ~2 ms without a new arrival and the rows re-run on the three-launch path --
+        bit-exact, one fallback, well under the ~1.3 s hand-off bound;
+      unchecked_async: groups of 64 consecutive blocks (the default map): groups 0-7 are
+        resident and complete, group 8 is dispatched into the slots they free and its census
+        completes then -- an oversized grid is slower, not failed: bit-exact, no fallback, no
+        pending error."""
     import time
     n, batch = 99991, 11
-    monkeypatch.setenv("HSFFT_BLUE_XCD", "9" if mode.startswith("refused") else "8")
-    if mode == "refused_coop":
-        monkeypatch.setenv("HSFFT_BX_COOP", "1")
-    if mode == "sync":
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "8" if mode == "sync" else "9")
+    if mode in ("sync", "census_sync"):
         monkeypatch.setenv("HSFFT_BX_SYNC", "1")
+    if mode in ("census_sync", "unchecked_async"):
+        monkeypatch.setenv("HSFFT_BX_UNCHECKED", "1")
+    if mode == "census_sync":
+        monkeypatch.setenv("HSFFT_BX_MAP", "0")
     x = T.complex_input(n, 0xC0C0, batch=batch).reshape(batch, n)
     ref = _oracle(x, 1, ("coop", n, batch))
     p = hsfft.Plan(n, 1)
@@ -251,7 +260,7 @@ def test_bluestein_persistent_launch_contract(mode, monkeypatch):
         hsfft.synchronize()
         dt = time.perf_counter() - t0
         assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), ref), (mode, it)
-        assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0 + (1 if mode.startswith("refused") else 0), mode
+        assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0 + (1 if mode in ("refused", "census_sync") else 0), mode
         assert dt < 0.5, f"{mode}: {dt:.3f} s for {batch} rows (a refused launch must not wait)"
     din.free()
     dout.free()
@@ -322,6 +331,71 @@ def test_bluestein_async_timeout_reported_once(monkeypatch):
         d.free()
     p.close()
     rp.close()
+    small.close()
+
+
+def test_bluestein_persistent_beside_concurrent_small_calls(monkeypatch):
+    """the persistent grid fills the chip (2 workgroups per CU x 256 CUs), and
+    the concurrent small fft_exec path launches one-workgroup kernels on per-thread streams
+    outside the device lock, so a small kernel can hold a slot the persistent grid needs.  One
+    thread runs asynchronous 99991-point batches (the persistent launch) while another issues
+    drop-in fft_exec calls of 1024 points throughout: no launch fell back, no error is pending,
+    every Bluestein output word equals the same rows run alone, sampled rows equal the oracle,
+    and every small call is bit-exact."""
+    import threading
+    monkeypatch.setenv("HSFFT_BLUE_XCD", "8")
+    n, batch, iters = 99991, 64, 6
+    L = hsfft.lib()
+    x = T.complex_input(n, 0x5EED, batch=batch).reshape(batch, n)
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    d_alone = hsfft.DeviceBuffer(x.nbytes)
+    d_conc = hsfft.DeviceBuffer(x.nbytes)
+    assert L.hsfft_synchronize() == 0
+    hsfft.exec_batched(p, din, d_alone, batch)
+    assert L.hsfft_synchronize() == 0
+    small = hsfft.Plan(1024, -1)
+    xs = [T.complex_input(1024, 0x600 + k) for k in range(4)]
+    refs = [T.oracle_c2c(v, -1) for v in xs]
+    stop = threading.Event()
+    errors, calls = [], [0]
+
+    def small_worker():
+        try:
+            L.hsfft_set_device(0)
+            k = 0
+            while not stop.is_set():
+                y = small.exec(xs[k % 4])
+                if not T.bits_equal(y, refs[k % 4]):
+                    errors.append(("small", k))
+                k += 1
+            calls[0] = k
+        except Exception as e:  # pragma: no cover
+            errors.append(("exception", repr(e)))
+
+    fb0 = L.hsfft_bluestein_fallbacks()
+    th = threading.Thread(target=small_worker)
+    th.start()
+    try:
+        for it in range(iters):
+            d_conc.fill_zero()
+            assert L.hsfft_exec_batched(p.ptr, hsfft.VP(din.ptr), hsfft.VP(d_conc.ptr), batch) == 0
+            assert L.hsfft_synchronize() == 0, (it, L.hsfft_last_error())
+            diff = hsfft.count_diff_words(d_alone, d_conc, x.nbytes)
+            assert diff == 0, (it, diff)
+    finally:
+        stop.set()
+        th.join(timeout=120)
+    assert not th.is_alive()
+    assert not errors, errors[:5]
+    assert calls[0] > 0
+    assert L.hsfft_bluestein_fallbacks() == fb0
+    y = d_alone.to_array(np.complex128).reshape(batch, n)
+    rows = [0, 37, batch - 1]
+    assert T.bits_equal(y[rows], _oracle(x[rows], 1, ("conc", n, 3)))
+    for d in (din, d_alone, d_conc):
+        d.free()
+    p.close()
     small.close()
 
 

@@ -21,7 +21,7 @@ import hsfft
 pytestmark = pytest.mark.gpu
 
 
-def run_two_ranks(tmp_path, config, batch):
+def run_two_ranks(tmp_path, config, batch, cpu=False):
     if hsfft.device_count() < 1:
         pytest.skip("no GPU")
     out = tmp_path / "rows"
@@ -29,17 +29,28 @@ def run_two_ranks(tmp_path, config, batch):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(T.REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--config", config, "--batch", str(batch), "--no-cpu-baseline", "--dump-rows", str(out)]
+           "--config", config, "--batch", str(batch), "--dump-rows", str(out)]
+    cmd += ["--cpu-seconds", "1"] if cpu else ["--no-cpu-baseline"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=T.REPO)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2, r.stdout[-2000:]  # rank 0 only, two ranks
     assert lines[0]["config"]["global_batch"] == 2 * batch
-    return out
+    return out, lines[0]
 
 
 def test_two_ranks_shard_rows_bit_exact(tmp_path):
-    out = run_two_ranks(tmp_path, "c2", 6)
+    """... and the N>1 line's own fields: every rank's ms per step and
+    roofline figures, the aggregate roofline against 2 x the peak, and the reference timed on the
+    host cores by rank 0 in the same run"""
+    out, line = run_two_ranks(tmp_path, "c2", 6, cpu=True)
+    per = line["per_rank"]
+    assert [p["rank"] for p in per] == [0, 1]
+    for p in per:
+        assert p["ms_per_step"] > 0 and p["event_ms_per_step"] > 0 and 0 < p["frac"] < 1
+    agg = line["roofline"]["aggregate"]
+    assert agg["peak"] == 16000.0 and 0 < agg["frac"] < 1
+    assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["cores"] >= 1
     seen = set()
     for rank in (0, 1):
         z = np.load(out / f"rank{rank}.npz")
@@ -53,7 +64,7 @@ def test_two_ranks_shard_rows_bit_exact(tmp_path):
 
 def test_two_ranks_r2c_chunked_shard_rows_bit_exact(tmp_path):
     """config 5's path (real rows of 2^22, output written chunk by chunk) sharded over two ranks"""
-    out = run_two_ranks(tmp_path, "c5", 2)
+    out, _ = run_two_ranks(tmp_path, "c5", 2)
     seen = set()
     for rank in (0, 1):
         z = np.load(out / f"rank{rank}.npz")

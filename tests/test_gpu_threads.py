@@ -148,3 +148,48 @@ def test_exec_multi_threads_single_device():
     y = dout.to_array(np.complex128).reshape(rows, n)
     assert T.bits_equal(y, T.oracle_c2c(x, 1))
     assert hsfft.lib().hsfft_exec_multi(p.ptr, ins, outs, rows, 99) < 0   # more devices than exist
+
+
+def test_thread_generations_recycle_resources():
+    """threads that come and go recycle the per-thread resources of the
+    lock-free small path (stream, page-locked slots, completion word) -- parked at exit, adopted
+    by the next thread, never created or destroyed on a live caller's path (round 5 reaped dead
+    threads' objects on a new thread's first call: +52 % per threaded call).  Three generations
+    of 8 threads call the drop-in fft_exec on one shared 1024-point plan (BASELINE config 1):
+    every output bit-exact vs the oracle, and the three generations create at most 8 streams."""
+    L = hsfft.lib()
+    n = 1024
+    plan = hsfft.Plan(n, 1)
+    xs = [T.complex_input(n, 0x7700 + t) for t in range(NTHREADS)]
+    refs = [T.oracle_c2c(x, 1) for x in xs]
+    errors = []
+    s0 = L.hsfft_thread_streams_created()
+
+    def worker(t, gen):
+        try:
+            L.hsfft_set_device(0)
+            for it in range(40):
+                y = np.zeros(n, dtype=np.complex128)
+                L.fft_exec(plan.ptr, T.ptr(xs[t]), T.ptr(y))
+                if not T.bits_equal(y, refs[t]):
+                    errors.append((gen, t, it, T.mismatches(y, refs[t])))
+        except Exception as e:  # pragma: no cover
+            errors.append(("exception", gen, t, repr(e)))
+
+    for gen in range(3):
+        start = threading.Barrier(NTHREADS)
+
+        def run(t, gen=gen, start=start):
+            start.wait()
+            worker(t, gen)
+
+        th = [threading.Thread(target=run, args=(t,)) for t in range(NTHREADS)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        assert not any(x.is_alive() for x in th)
+    made = L.hsfft_thread_streams_created() - s0
+    assert not errors, errors[:10]
+    assert made <= NTHREADS, f"three generations of {NTHREADS} threads created {made} streams"
+    plan.close()

@@ -76,7 +76,8 @@ def _metadata():
             cur = m.group(1)
             kernels.setdefault(cur, {})
             continue
-        m = re.match(r"\s+\.(vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|sgpr_count):\s+(\d+)", line)
+        m = re.match(r"\s+\.(vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|sgpr_count|group_segment_fixed_size):"
+                     r"\s+(\d+)", line)
         if m and cur:
             kernels[cur][m.group(1)] = int(m.group(2))
     return kernels
@@ -119,7 +120,13 @@ def test_no_wrong_result_probes_in_product():
                   # forms and walk orders, walk2's phase trace
                   b"HSFFT_R2C_OVL", b"HSFFT_R2C_PFH", b"HSFFT_R2C_ORDER", b"HSFFT_R2C_DEBUG",
                   # round 5's per-CU store token (the store-burst alignment test)
-                  b"HSFFT_R2C_STOK"):
+                  b"HSFFT_R2C_STOK",
+                  # round 6: the chunked two-stream MALL pipeline and its row
+                  # count / lag (52-67 vs 91 GSamples/s), the dead non-temporal pass knob, the
+                  # merged acquire (+3.9 %), the event-polling small-call wait (no faster) -- and
+                  # the cooperative launch, which crashed profiled processes at exit
+                  b"HSFFT_PIPE", b"HSFFT_MALL_ROWS", b"HSFFT_NT\0", b"HSFFT_BX_MERGE", b"HSFFT_SMALL_SPIN",
+                  b"HSFFT_BX_COOP", b"hipLaunchCooperativeKernel"):
         assert probe not in blob, probe
     names = _metadata()
     bad = [k for k in names
@@ -133,3 +140,39 @@ def test_no_wrong_result_probes_in_product():
            or re.match(r"^_ZN2r810k_r2c_last", k)
            or re.match(r"^_ZN2mr6k_row2I.*ELi3EEEvNS_5MArgsE$", k)]
     assert not bad, bad
+
+
+def _bx_lds_bytes():
+    """bxc::LDS_BYTES, the dynamic LDS the host launches k_bxcd with (csrc/hsfft_blue_xcd.h)"""
+    src = open(os.path.join(REPO, "mixed-radix-fast-fourier-transform_amd", "csrc", "hsfft_blue_xcd.h")).read()
+    m = re.search(r"constexpr size_t LDS_BYTES = ([^;]+);", src)
+    assert m, "LDS_BYTES not found"
+    expr = m.group(1).replace("(size_t)", "")
+    assert re.fullmatch(r"[0-9+*() ]+", expr), expr
+    return eval(expr)  # noqa: S307 -- digits and + * ( ) only, checked above
+
+
+def test_persistent_bluestein_grid_is_coresident():
+    """the persistent Bluestein launch (c4) assumes 2 workgroups of 512
+    threads per CU -- 8 waves per CU, i.e. 2 waves per SIMD, times the 2 workgroups: every limit
+    must allow 4 waves per SIMD.  The occupancy API the host asks can over-report by one block per
+    CU at some SGPR counts (MI355X_MICROARCH.md), so the budget is checked here from the code
+    object with the guide's formulas: VGPRs (above), SGPRs -- waves/SIMD = floor(800 /
+    (ceil(sgpr/16)*16 + 16)) >= 4, i.e. at most 176 SGPRs -- and LDS: two workgroups' static +
+    dynamic LDS within the CU's 160 KiB."""
+    kernels = _metadata()
+    hits = {k: v for k, v in kernels.items() if re.match(r"^_ZN3bxc6k_bxcdILin?1EEE", k)}
+    assert len(hits) == 2, hits
+    lds = _bx_lds_bytes()
+    for name, res in hits.items():
+        sg = res["sgpr_count"]
+        assert 800 // (-(-sg // 16) * 16 + 16) >= 4, (name, res)
+        assert 2 * (lds + res.get("group_segment_fixed_size", 0)) <= 160 * 1024, (name, res, lds)
+        regs = res.get("vgpr_count", 0) + res.get("agpr_count", 0)
+        assert waves_per_simd(regs) >= 4, (name, res)
+
+
+def test_sgpr_formula_boundary():
+    """the formula above: 176 SGPRs still allow 4 waves per SIMD, 177 do not"""
+    f = lambda sg: 800 // (-(-sg // 16) * 16 + 16)
+    assert f(176) == 4 and f(177) == 3 and f(101) >= 4

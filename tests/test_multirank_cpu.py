@@ -53,6 +53,18 @@ def test_bench_multirank_dry_run(nproc, launcher):
     for r in range(nproc):
         assert out["rank_checksums"][r] == pytest.approx(expected_checksum(n, r * batch, batch), rel=1e-12)
     assert out["value"] > 0 and out["ms_per_step"] > 0
+    # the N>1 line carries every rank's own numbers, the aggregate roofline
+    # and the reference timed on the host cores in the same run (rank 0, after the timed region)
+    per = out["per_rank"]
+    assert [p["rank"] for p in per] == list(range(nproc))
+    for p in per:
+        assert p["ms_per_step"] > 0 and p["event_ms_per_step"] > 0 and p["achieved"] > 0 and p["frac"] > 0
+    assert max(p["ms_per_step"] for p in per) == pytest.approx(out["ms_per_step"], rel=1e-3)
+    agg = out["roofline"]["aggregate"]
+    assert agg["peak"] == 8000.0 * nproc and agg["achieved"] > 0
+    assert agg["frac"] == pytest.approx(agg["achieved"] / agg["peak"], abs=1e-4)
+    cb = out["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("reference", "port") and cb["unit"] == "GSamples/s"
 
 
 def test_row_range_partition():
