@@ -115,9 +115,11 @@ int hsfft_bench_copy(const void *d_src, void *d_dst, size_t bytes, int iters, fl
  * be resident at once; the library checks that with the occupancy API before launching, and a
  * grid that cannot be co-resident runs on the three-launch path at once (same results, more
  * time).  Its in-launch waits keep a last-resort bound (~1.3 s without progress):
- *   - synchronous entry points (fft_exec, fft_r2c_exec / fft_c2r_exec, hsfft_exec_batched_host,
- *     hsfft_exec_multi) wait for the launch and re-run the rows of a launch whose waits timed
- *     out on the three-launch path themselves;
+ *   - synchronous entry points (fft_exec, fft_r2c_exec / fft_c2r_exec, hsfft_exec_multi) wait
+ *     for the launch and re-run the rows of a launch whose waits timed out on the three-launch
+ *     path themselves; hsfft_exec_batched_host keeps its launches asynchronous (uploads overlap
+ *     transforms), checks its own error word once at the end and then re-runs the whole batch
+ *     on the three-launch path;
  *   - asynchronous device-buffer calls (hsfft_exec_batched, hsfft_r2c_batched, ...) record a
  *     timed-out wait in an error word of the CALLING THREAD; it is reported exactly once, as
  *     HSFFT_ERR_DEVICE, by that thread's next hsfft_synchronize() on that device (or its next

@@ -665,7 +665,7 @@ static size_t g_pl_bytes[HS_MAX_DEV];
  * library stream, behind those launches, before the new owner's first launch (pl_words), or at
  * the new owner's first report (pl_report, after the stream was waited for). */
 struct PlErr {
-    unsigned *dev;  /* 64 words on the device: [0] async sticky, [32] sync */
+    unsigned *dev;  /* 64 words on the device: [0] async sticky, [16] deferred, [32] sync */
     unsigned *host; /* 64 page-locked words: copies of the same */
     bool inherited;
 };
@@ -675,10 +675,10 @@ static int pl_words(int dev, PlErr **out)
 {
     PlErr *p = &t_pl[dev];
     if (p->dev && p->inherited) {
-        /* the exited owner's asynchronous launches ran on the library stream: clear word 0 and
-         * its host copy behind them */
-        HCHK(hipMemsetAsync(p->dev, 0, sizeof(unsigned), primary()));
-        HCHK(hipMemcpyAsync(p->host, p->dev, sizeof(unsigned), hipMemcpyDeviceToHost, primary()));
+        /* the exited owner's asynchronous / deferred launches ran on the library stream: clear
+         * words 0..31 (async 0, deferred 16) and their host copies behind them */
+        HCHK(hipMemsetAsync(p->dev, 0, 32 * sizeof(unsigned), primary()));
+        HCHK(hipMemcpyAsync(p->host, p->dev, 32 * sizeof(unsigned), hipMemcpyDeviceToHost, primary()));
         p->inherited = false;
     }
     if (!p->dev) {
@@ -731,6 +731,18 @@ static int pl_report(void)
              "thread's Bluestein calls since its last hsfft_synchronize() on this device are invalid "
              "(HSFFT_BX_SYNC=1 re-runs such rows automatically)", w);
     return -2;
+}
+
+int hsd_blue_deferred_take(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= HS_MAX_DEV) return 0;
+    PlErr *p = &t_pl[dev];
+    if (!p->host || *(volatile unsigned *)(p->host + 16) == 0) return 0;
+    *(volatile unsigned *)(p->host + 16) = 0;
+    (void)hipMemsetAsync(p->dev + 16, 0, sizeof(unsigned), primary());
+    (void)hipStreamSynchronize(primary());
+    return 1;
 }
 
 /* wait for the library stream; a pending persistent-launch error stays pending */
@@ -805,8 +817,11 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     unsigned *ctr = g_pl_ctr[dev];
     /* the counters are zeroed before every launch (Guideline 16, re-initialise every call) */
     HCHK(hipMemsetAsync(ctr, 0, need, stream()));
-    unsigned *err = sync ? pe->dev + 32 : pe->dev;
-    if (sync) HCHK(hipMemsetAsync(err, 0, sizeof(unsigned), stream()));
+    /* word: [0] asynchronous (sticky, hsd_sync_report), [16] deferred (cumulative until
+     * hsd_blue_deferred_take), [32] synchronous (cleared per launch) */
+    const int wi = sync == 1 ? 32 : sync == 2 ? 16 : 0;
+    unsigned *err = pe->dev + wi;
+    if (sync == 1) HCHK(hipMemsetAsync(err, 0, sizeof(unsigned), stream()));
     bxc::XArgs a;
     memset(&a, 0, sizeof a);
     a.in = (const double2 *)in;
@@ -823,7 +838,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     a.ng = (unsigned)ng;
     a.nsig = (unsigned)nsig;
     a.tlimit = bxc::T_LIMIT;
-    a.climit = sync ? bxc::C_LIMIT : bxc::T_LIMIT; /* fail fast only where the caller re-runs the rows */
+    a.climit = sync ? bxc::C_LIMIT : bxc::T_LIMIT; /* fail fast only where the caller re-runs the rows (1, 2) */
     {
         /* polls of the hand-off counters 4 x s_sleep 2 apart (was 1): in-process A/B on two boxes
          * 32.51 vs 32.61 and 32.13 vs 32.29 ms per 8192 rows (profiles/r05e_*, r05g_*) */
@@ -844,15 +859,14 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     if (dbg) {
         if (!s_dbg[dev]) HCHK(hipMalloc((void **)&s_dbg[dev], 4096 * 8 * sizeof(unsigned)));
         HCHK(hipMemsetAsync(s_dbg[dev], 0, (size_t)grid * 8 * sizeof(unsigned), stream()));
-        a.dbg = s_dbg[dev];
-        sync = 1;
+        a.dbg = s_dbg[dev]; /* the call waits for the trace (its error word keeps its own contract) */
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), bxc::LDS_BYTES, stream(), a);
     HCHK(hipGetLastError());
-    /* host copy of the word this launch could set (async: the cumulative sticky word) */
-    unsigned *hw = sync ? pe->host + 32 : pe->host;
+    /* host copy of the word this launch could set (async / deferred: cumulative words) */
+    unsigned *hw = pe->host + wi;
     HCHK(hipMemcpyAsync(hw, err, sizeof(unsigned), hipMemcpyDeviceToHost, stream()));
-    if (!sync) return 0;
+    if (sync != 1 && !dbg) return 0;
     HCHK(hipStreamSynchronize(stream()));
     const unsigned w = *(volatile unsigned *)hw;
     if (dbg) { /* mean us per row: P1, wait A, P2, wait B, P3 */
@@ -868,7 +882,7 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
                 grid, t[0] / grid, t[1] / rows / 100.0, t[6] / rows / 100.0, t[2] / rows / 100.0, t[3] / rows / 100.0,
                 t[7] / rows / 100.0, t[4] / rows / 100.0, t[5] / rows / 100.0);
     }
-    if (w) { /* the caller re-runs the rows */
+    if (sync == 1 && w) { /* the caller re-runs the rows */
         *(volatile unsigned *)hw = 0;
         snprintf(g_err, sizeof g_err, "hsd_blue_xcd: an in-launch wait timed out (error word %u)", w);
         return 2;

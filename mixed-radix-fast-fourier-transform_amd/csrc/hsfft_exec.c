@@ -36,6 +36,13 @@ static __thread int t_sync_call;
 
 void hs_sync_call(int enter) { t_sync_call += enter ? 1 : -1; }
 
+/* > 0 inside hsfft_exec_batched_host's pipeline: its persistent Bluestein launches
+ * stay asynchronous -- so chunk k+1's upload overlaps chunk k's transform -- and record a
+ * timed-out wait in the thread's DEFERRED error word, which the pipeline reads once after its
+ * final stream wait; a set word re-runs the whole batch on the three-launch path (t_no_xcd) */
+static __thread int t_deferred_call;
+static __thread int t_no_xcd;
+
 /* per-device API locks (recursive: public entry points call each other) */
 static pthread_mutex_t g_dev_mtx[HS_MAX_DEV];
 static pthread_once_t g_dev_once = PTHREAD_ONCE_INIT;
@@ -983,9 +990,9 @@ static int run_bluestein(hs_entry *e, hs_devstate *ds, const void *in, long long
      * and a launch whose waits timed out makes its rows run on the three-launch path as well.
      * Both count as fallbacks. */
     const int ng = env_int("HSFFT_BLUE_XCD", 8);
-    const int sync = t_sync_call > 0 || env_int("HSFFT_BX_SYNC", 0);
+    const int sync = t_sync_call > 0 || env_int("HSFFT_BX_SYNC", 0) ? 1 : t_deferred_call > 0 ? 2 : 0;
     long long done = 0;
-    if (fuse && ng > 0) {
+    if (fuse && ng > 0 && !t_no_xcd) {
         thread_resources_used(hsd_get_device()); /* this thread's error words are recycled when it exits */
         const size_t ib = (size_t)ng * 4 * sizeof(fft_data) * (size_t)M; /* 4 images per group */
         void *img = hs_scratch(3, ib);
@@ -1441,9 +1448,20 @@ int hsfft_exec_batched_host(fft_object obj, const fft_data *h_in, fft_data *h_ou
     if (rc) return rc;
     const int d = hs_lock_device();
     hs_entry *e = hs_entry_get(obj);
-    t_sync_call++;
+    (void)hsd_blue_deferred_take(); /* a word an earlier, failed pipeline left set (the stream is idle) */
+    t_deferred_call++;
     rc = e ? exec_host_locked(obj, e, h_in, h_out, batch) : HSFFT_ERR_ARG;
-    t_sync_call--;
+    t_deferred_call--;
+    if (rc == 0 && e && hsd_blue_deferred_take()) {
+        /* a persistent Bluestein launch of the pipeline timed out (its waits, or its census): the
+         * whole batch again, every Bluestein row on the three-launch path */
+        __atomic_fetch_add(&g_blue_fallbacks, 1, __ATOMIC_RELAXED);
+        t_no_xcd++;
+        t_sync_call++;
+        rc = exec_host_locked(obj, e, h_in, h_out, batch);
+        t_sync_call--;
+        t_no_xcd--;
+    }
     hs_entry_put(e);
     hs_unlock_device(d);
     return rc;

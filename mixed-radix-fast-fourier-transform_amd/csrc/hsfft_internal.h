@@ -132,12 +132,16 @@ int mr_has_variant(const hsd_pass *p);
  * h+1 bins (hsfft_r2c_batched_compact) instead of the mirrored N */
 int hsd_r2c_last(const void *Z, long long zdist, void *X, long long xdist, const void *tw, const void *w2, long long h,
                  long long B, int batch, int sgn, int compact);
-/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h), asynchronous unless `sync`:
+/* Bluestein M = 2^18 in one persistent launch (hsfft_blue_xcd.h); sync 0 asynchronous, 1
+ * synchronous, 2 deferred (asynchronous, the outcome read later by hsd_blue_deferred_take):
  * 0 queued / done, 1 not applicable, 2 (sync) in-launch waits timed out, 3 grid not co-resident
  * (re-run the rows elsewhere in both), < 0 HIP error.  Asynchronous: a timed-out wait is
  * reported by the launching thread's next hsd_sync_report. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
                  const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng, int sync);
+/* 1 if a deferred launch (sync 2) of this thread on the current device timed out since the last
+ * call (call after waiting for the library stream); clears the word */
+int hsd_blue_deferred_take(void);
 /* Bluestein M = 2^18: forward last pass + hk product + inverse first pass in one kernel */
 int hsd_blue_mid(const void *in, void *out, long long dist, const void *tw, const void *hk, int batch, int sgn,
                  int conj, int dir, int sgn2, int conj2); /* hsfft_pass_mr.h has a kernel for this pass */

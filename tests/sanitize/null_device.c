@@ -315,6 +315,13 @@ int hsd_blue_first(const void *in, long long idist, void *out, long long odist, 
  * next hsd_sync_report; 2: the grid is refused as not co-resident (3) -- the host's three-launch
  * path runs */
 int null_bx_timeout;
+static __thread int deferred_pending;
+int hsd_blue_deferred_take(void)
+{
+    const int v = deferred_pending;
+    deferred_pending = 0;
+    return v;
+}
 
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
                  const void *hk, void *img, size_t img_bytes, long long nsig, int batch, int sgn, int ng, int sync)
@@ -325,8 +332,9 @@ int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, co
     touch_rows_w(img, 0, (long long)(img_bytes / 16), 1, 16);
     if (null_bx_timeout == 2) return 3;
     if (null_bx_timeout == 1) {
-        if (sync) return 2;
-        pl_pending = 1;
+        if (sync == 1) return 2;
+        if (sync == 2) deferred_pending = 1; /* read by hsd_blue_deferred_take */
+        else pl_pending = 1;
         return 0;
     }
     touch_rows_w(out, odist, nsig, batch, 16);

@@ -134,8 +134,13 @@ def test_host_batched_pipeline_bit_exact(n, batch, chunk_mb, monkeypatch):
     monkeypatch.setenv("HSFFT_HOST_CHUNK_MB", chunk_mb)
     x = T.complex_input(n, 0xAB ^ n, batch=batch).reshape(batch, n)
     p = hsfft.Plan(n, 1)
+    fb0 = hsfft.lib().hsfft_bluestein_fallbacks()
     y = hsfft.exec_batched_host(p, x)
     assert T.bits_equal(y, T.oracle_c2c(x, 1)), n
+    # 99991: the pipeline's persistent launches run deferred (asynchronous, one check at the end,
+    # round 6) -- none fell back, nothing is left pending
+    assert hsfft.lib().hsfft_bluestein_fallbacks() == fb0
+    assert hsfft.lib().hsfft_synchronize() == 0
     p.close()
 
 
@@ -326,6 +331,14 @@ def test_bluestein_async_timeout_reported_once(monkeypatch):
     y1 = p.exec(x[3])  # the drop-in fft_exec on host buffers is synchronous by itself
     assert L.hsfft_bluestein_fallbacks() == fb1 + 2
     assert T.bits_equal(y1, ref[3])
+    assert L.hsfft_synchronize() == 0
+    # 5. the host pipeline keeps its launches asynchronous and reads its own DEFERRED error word
+    # once at the end (round 6): the timed-out batch re-runs on the three-launch path
+    # -- bit-exact, one fallback, nothing left for hsfft_synchronize()
+    monkeypatch.setenv("HSFFT_HOST_CHUNK_MB", "4")  # 3 chunks of 2 rows + 2
+    yh = hsfft.exec_batched_host(p, x)
+    assert L.hsfft_bluestein_fallbacks() == fb1 + 3
+    assert T.bits_equal(yh, ref)
     assert L.hsfft_synchronize() == 0
     for d in (din, dout, dxr, dyr):
         d.free()
