@@ -938,7 +938,7 @@ void hsd_thread_park(int dev, const hsd_tset *h)
     TSet s;
     s.own = t_own[dev];
     s.pl = t_pl[dev];
-    s.h = h ? *h : hsd_tset{{nullptr, nullptr}, 0, nullptr};
+    s.h = h ? *h : hsd_tset{{nullptr, nullptr}, 0, nullptr, 0};
     t_own[dev] = 0;
     t_pl[dev] = PlErr{nullptr, nullptr, false};
     if (!s.own && !s.pl.dev && !s.h.pin[0] && !s.h.pin[1] && !s.h.flag) return;

@@ -1201,7 +1201,11 @@ static __thread void *t_pin[HS_MAX_DEV][2];
 static __thread size_t t_pin_sz[HS_MAX_DEV];
 /* this thread's completion word per device (page-locked) and its sequence */
 static __thread unsigned *t_flag[HS_MAX_DEV];
-static __thread unsigned t_seq;
+/* the value this thread's next completion word on device d must reach: it travels WITH the word
+ * when a set is parked and adopted (a new owner restarting at 1 would take the previous owner's
+ * last value, if it was 1, for its own first completion -- round 6, caught by
+ * test_thread_generations_recycle_resources) */
+static __thread unsigned t_seq[HS_MAX_DEV];
 
 /* Per-thread resources (page-locked slots, completion words, the thread's own streams and
  * persistent-launch error words) are recycled, not destroyed, when the thread exits: a pthread
@@ -1218,7 +1222,7 @@ static void thread_resources_free(void *unused)
 {
     (void)unused;
     for (int d = 0; d < HS_MAX_DEV; d++) {
-        const hsd_tset h = {{t_pin[d][0], t_pin[d][1]}, t_pin_sz[d], t_flag[d]};
+        const hsd_tset h = {{t_pin[d][0], t_pin[d][1]}, t_pin_sz[d], t_flag[d], t_seq[d]};
         hsd_thread_park(d, &h);
         t_pin[d][0] = t_pin[d][1] = NULL;
         t_pin_sz[d] = 0;
@@ -1257,6 +1261,7 @@ static void thread_resources_used(int d)
         t_pin[d][1] = h.pin[1];
         t_pin_sz[d] = h.pin_sz;
         t_flag[d] = h.flag;
+        t_seq[d] = h.seq; /* the word holds the previous owner's last value: continue after it */
     }
 }
 
@@ -1300,16 +1305,20 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
         }
     }
     const int fmode = env_int("HSFFT_SMALL_FLAG", 2);
-    if (!t_flag[d] && fmode) t_flag[d] = (unsigned *)hsd_host_alloc(64);
+    if (!t_flag[d] && fmode) {
+        t_flag[d] = (unsigned *)hsd_host_alloc(64);
+        if (t_flag[d]) memset(t_flag[d], 0, 64); /* no stale value can match the next sequence */
+        t_seq[d] = 0;
+    }
     const int use_flag = fmode >= 1 && t_flag[d] != NULL; /* the mode of THIS call, not of the first */
     memcpy(t_pin[d][0], inp, bytes);
     hsd_select_stream(3);
     t_done_armed = 0;
     if (use_flag) {
-        if (++t_seq == 0) t_seq = 1;
+        if (++t_seq[d] == 0) t_seq[d] = 1;
         if (fmode >= 2) { /* a one-workgroup kernel stores the word itself */
             t_done = t_flag[d];
-            t_done_val = t_seq;
+            t_done_val = t_seq[d];
         }
     }
     int rc = run_chain(e, ds, t_pin[d][0], obj->N, t_pin[d][1], obj->N, 1, e->sgn, 0, e->sgn, HS_LOAD_PLAIN, NULL,
@@ -1319,8 +1328,8 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
         /* completion seen through a host word instead of the stream wait: stored by the
          * kernel (HSFFT_SMALL_FLAG=2, one-workgroup launches), else by the command processor
          * after the kernel (1); 0: the stream wait */
-        if (use_flag && t_done_armed) rc = hsd_host_word_wait(t_flag[d], t_seq);
-        else if (use_flag) rc = hsd_stream_signal_wait(t_flag[d], t_seq);
+        if (use_flag && t_done_armed) rc = hsd_host_word_wait(t_flag[d], t_seq[d]);
+        else if (use_flag) rc = hsd_stream_signal_wait(t_flag[d], t_seq[d]);
         else rc = hsd_stream_sync();
     }
     if (rc) hsd_stream_sync(); /* nothing of this call may still run when the pin is dropped */

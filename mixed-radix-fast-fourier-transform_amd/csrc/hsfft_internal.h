@@ -113,6 +113,7 @@ typedef struct {
     void *pin[2];     /* page-locked in / out slots of the small path (hsd_host_alloc) */
     size_t pin_sz;    /* bytes of each slot */
     unsigned *flag;   /* page-locked completion word (hsd_host_alloc) */
+    unsigned seq;     /* the last value the word was set to (the next owner continues after it) */
 } hsd_tset;
 void hsd_thread_park(int dev, const hsd_tset *h); /* thread exit: this thread's set of `dev` */
 int hsd_thread_adopt(int dev, hsd_tset *h);       /* 1: a parked set was taken (host part in *h) */

@@ -96,9 +96,11 @@ int hsd_d2h_async(void *h, const void *d, size_t bytes) { return hsd_d2h(h, d, b
 int hsd_stream_sync(void) { return 0; }
 int hsd_host_word_wait(unsigned *flag, unsigned v)
 {
-    (void)flag;
-    (void)v;
-    return 0; /* never armed on the null device */
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) {
+        snprintf(err, sizeof err, "null device: completion word %u, awaited %u", *flag, v);
+        return -1;
+    }
+    return 0;
 }
 int hsd_stream_signal_wait(unsigned *flag, unsigned v)
 {
@@ -262,6 +264,17 @@ int hsd_run_pass(const hsd_pass *p, const hsd_launch *l)
     if (sidx == 3) {
         own_stream_used();
         usleep(20);
+    }
+    /* a one-workgroup launch that stores its completion word itself (the small path): the word
+     * must not ALREADY hold the awaited value -- the host would see "done" before the kernel ran
+     * (a recycled word must continue its previous owner's sequence) */
+    if (l->done) {
+        if (__atomic_load_n(l->done, __ATOMIC_ACQUIRE) == l->done_val) {
+            snprintf(err, sizeof err, "null device: completion word already holds the awaited value %u", l->done_val);
+            return -1;
+        }
+        __atomic_store_n(l->done, l->done_val, __ATOMIC_RELEASE);
+        if (l->armed) *l->armed = 1;
     }
     const long long M = (long long)p->P * p->A * p->B;
     const long long in_len = l->load_op == HS_LOAD_CHIRP ? l->nsig : M;

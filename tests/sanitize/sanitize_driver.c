@@ -160,11 +160,11 @@ static fft_object g_small;
 
 static void *small_caller(void *arg)
 {
-    const int refresher = (int)(long)arg;
+    const int refresher = (int)(long)arg == 1, calls = (int)(long)arg >= 2 ? (int)(long)arg - 1 : 300;
     fft_data *x = cbuf(1024), *y = cbuf(1024);
     null_mark_host(x, 1);
     null_mark_host(y, 1);
-    for (int it = 0; it < 300; it++) {
+    for (int it = 0; it < calls; it++) {
         if (refresher) CHECK(hsfft_plan_refresh(g_small) == 0, "refresh while small calls run");
         fft_exec(g_small, x, y);
     }
@@ -334,6 +334,13 @@ int main(void)
             for (long t = 0; t < 8; t++) pthread_create(&st[t], NULL, small_caller, (void *)0L);
             for (int t = 0; t < 8; t++) pthread_join(st[t], NULL);
             if (gen == 0) allocs_gen1 = __atomic_load_n(&null_host_allocs, __ATOMIC_RELAXED);
+        }
+        /* 5b'. threads that make exactly ONE call, then threads that make two: a recycled
+         * completion word continues its previous owner's sequence (a new owner restarting at 1
+         * would find 1 already there and take it for its own kernel's completion) */
+        for (int gen = 0; gen < 2; gen++) {
+            for (long t = 0; t < 8; t++) pthread_create(&st[t], NULL, small_caller, (void *)(gen ? 3L : 2L));
+            for (int t = 0; t < 8; t++) pthread_join(st[t], NULL);
         }
         const long long made = hsfft_thread_streams_created() - str0;
         CHECK(made <= 8 - 4 && made >= 0, "three generations of 8 threads created %lld streams (4 parked sets existed)", made);
