@@ -156,7 +156,10 @@ def test_thread_generations_recycle_resources():
     by the next thread, never created or destroyed on a live caller's path (round 5 reaped dead
     threads' objects on a new thread's first call: +52 % per threaded call).  Three generations
     of 8 threads call the drop-in fft_exec on one shared 1024-point plan (BASELINE config 1):
-    every output bit-exact vs the oracle, and the three generations create at most 8 streams."""
+    every output bit-exact vs the oracle, and the three generations create at most 8 streams.
+    Then generations whose threads make exactly ONE call, then two: a recycled completion word
+    must continue its previous owner's sequence (round 6: a new owner restarting at 1 found 1
+    already in the word and copied its output before its kernel had run)."""
     L = hsfft.lib()
     n = 1024
     plan = hsfft.Plan(n, 1)
@@ -165,10 +168,10 @@ def test_thread_generations_recycle_resources():
     errors = []
     s0 = L.hsfft_thread_streams_created()
 
-    def worker(t, gen):
+    def worker(t, gen, calls):
         try:
             L.hsfft_set_device(0)
-            for it in range(40):
+            for it in range(calls):
                 y = np.zeros(n, dtype=np.complex128)
                 L.fft_exec(plan.ptr, T.ptr(xs[t]), T.ptr(y))
                 if not T.bits_equal(y, refs[t]):
@@ -176,12 +179,12 @@ def test_thread_generations_recycle_resources():
         except Exception as e:  # pragma: no cover
             errors.append(("exception", gen, t, repr(e)))
 
-    for gen in range(3):
+    for gen, calls in enumerate([40, 40, 40, 1, 2, 1, 3]):
         start = threading.Barrier(NTHREADS)
 
-        def run(t, gen=gen, start=start):
+        def run(t, gen=gen, start=start, calls=calls):
             start.wait()
-            worker(t, gen)
+            worker(t, gen, calls)
 
         th = [threading.Thread(target=run, args=(t,)) for t in range(NTHREADS)]
         for x in th:
@@ -191,5 +194,5 @@ def test_thread_generations_recycle_resources():
         assert not any(x.is_alive() for x in th)
     made = L.hsfft_thread_streams_created() - s0
     assert not errors, errors[:10]
-    assert made <= NTHREADS, f"three generations of {NTHREADS} threads created {made} streams"
+    assert made <= NTHREADS, f"seven generations of {NTHREADS} threads created {made} streams"
     plan.close()
