@@ -12,7 +12,8 @@ Variants: pf::k_r2c_walk2 (round 3's one-per-CU split walk; HSFFT_R2C_WALK=2) wi
 lengths and orders; k_r2c_walk1's other prefetch forms (HSFFT_R2C_PFH 0 / 2 / 3) and walk
 orders (HSFFT_R2C_ORDER) and its per-CU store token (HSFFT_R2C_STOK); round 1's split kernel r8::k_r2c_last (HSFFT_R2C_FUSE=2); pass A and
 the split walk overlapped over sub-chunks (HSFFT_R2C_OVL); the c3 row kernel's stage-5 twiddles
-of steps 1-3 through LDS (HSFFT_ROW_TWN=3).  Bit-exact vs the oracle.
+of steps 1-3 through LDS (HSFFT_ROW_TWN=3); since round 6 the chunked two-stream pipeline of
+two-pass plans (HSFFT_PIPE, HSFFT_MALL_ROWS, HSFFT_PIPE_LAG).  Bit-exact vs the oracle.
 """
 import numpy as np
 import pytest
@@ -120,3 +121,24 @@ def test_r2c_walk1_store_token(n, sgn, batch, stok, monkeypatch):
     monkeypatch.setenv("HSFFT_R2C_STOK", stok)
     y, ref = _r2c(n, sgn, batch, 37)
     assert T.bits_equal(y, ref)
+
+
+@pytest.mark.parametrize("rows,lag", [("2", "2"), ("1", "1"), ("3", "2")])
+def test_mall_pipeline(rows, lag, monkeypatch):
+    """round 6: the chunked two-stream pipeline of two-pass plans (HSFFT_PIPE with
+    HSFFT_MALL_ROWS rows per chunk and HSFFT_PIPE_LAG chunks ahead; measured 52-67 vs 91
+    GSamples/s on c2, development build only) -- bit-exact vs the oracle on 2^20, odd batch"""
+    monkeypatch.setenv("HSFFT_PIPE", "1")
+    monkeypatch.setenv("HSFFT_MALL_ROWS", rows)
+    monkeypatch.setenv("HSFFT_PIPE_LAG", lag)
+    n, batch = 1 << 20, 5
+    x = T.complex_input(n, 0x9191, batch=batch).reshape(batch, n)
+    p = hsfft.Plan(n, 1)
+    din = hsfft.DeviceBuffer.from_array(x)
+    dout = hsfft.DeviceBuffer(x.nbytes)
+    hsfft.exec_batched(p, din, dout, batch)
+    hsfft.synchronize()
+    assert T.bits_equal(dout.to_array(np.complex128).reshape(batch, n), T.oracle_c2c(x, 1))
+    din.free()
+    dout.free()
+    p.close()
