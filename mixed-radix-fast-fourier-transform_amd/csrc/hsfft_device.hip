@@ -660,10 +660,13 @@ static size_t g_pl_bytes[HS_MAX_DEV];
  * calls), so no other synchronisation -- a scratch pool growing, a device state being built, an
  * unrelated plan's call, another thread -- can consume or inherit it.  The synchronous word is
  * cleared before every synchronous launch and read right after it (hsd_blue_xcd returns 2).
+ * The deferred word (16) is the host pipeline's (hsfft_exec_batched_host): cumulative over the
+ * pipeline's launches, read and cleared once after its final stream wait (hsd_blue_deferred_take).
  * Words adopted from an exited thread (hsd_thread_adopt) are `inherited`: whatever that thread's
- * asynchronous launches left in word 0 is discarded, never reported to the new owner -- on the
- * library stream, behind those launches, before the new owner's first launch (pl_words), or at
- * the new owner's first report (pl_report, after the stream was waited for). */
+ * asynchronous or deferred launches left in words 0 / 16 is discarded, never reported to the new
+ * owner -- on the library stream, behind those launches, before the new owner's first launch
+ * (pl_words), or at its first report (pl_report, after the stream was waited for; a deferred
+ * word is also discarded at the start of every host pipeline). */
 struct PlErr {
     unsigned *dev;  /* 64 words on the device: [0] async sticky, [16] deferred, [32] sync */
     unsigned *host; /* 64 page-locked words: copies of the same */
@@ -762,15 +765,18 @@ int hsd_sync_report(void)
 /* Bluestein M = 2^18 as one persistent launch (hsfft_blue_xcd.h).  img: ng x 4 x M points of
  * scratch.  Every workgroup must be resident at once: the occupancy API is asked on the host
  * and a grid that does not fit is refused (returned as 3: the caller runs the three-launch
- * path at once); inside the launch a per-group arrival census proves it (a synchronous call's
- * grid the API over-promised fails in ~2 ms, as a timed-out launch).  (Round 4's hipLaunchCooperativeKernel form crashed
- * profiled processes at exit; removed in round 6.)  HSFFT_BX_UNCHECKED=1
- * (tests only) skips the host check, so that the census has to catch an oversized grid.
+ * path at once); inside the launch a per-group arrival census proves it (in a synchronous or
+ * deferred call a group the API over-promised fails in ~2 ms, as a timed-out launch).  (Round
+ * 4's cooperative-launch form crashed profiled processes at exit; removed
+ * in round 6.)  HSFFT_BX_UNCHECKED=1 (tests only) skips the host check, so that the census has
+ * to catch an oversized grid.
  * Asynchronous (sync == 0): the launch is queued on the library stream with a copy of this
  * thread's sticky error word behind it; a wait that still timed out (the last-resort bound,
  * ~1.3 s without progress; HSFFT_BX_TLIMIT ticks of the 100 MHz counter for tests) is reported
- * by this thread's next hsd_sync_report().  Synchronous (sync != 0): the call waits, and a
- * timed-out launch returns 2 so the caller re-runs its rows on the three-launch path.
+ * by this thread's next hsd_sync_report().  Synchronous (sync == 1): the call waits, and a
+ * timed-out launch returns 2 so the caller re-runs its rows on the three-launch path.  Deferred
+ * (sync == 2): queued like an asynchronous launch, its outcome in the deferred word, which the
+ * caller reads with hsd_blue_deferred_take() after its own final stream wait.
  * Returns 0 on success (queued), 1 if not applicable, 2 (sync) if an in-launch wait timed out,
  * 3 if the grid cannot be co-resident, < 0 on a HIP error. */
 int hsd_blue_xcd(const void *in, long long idist, void *out, long long odist, const void *tw, const void *chirp,
