@@ -102,6 +102,14 @@ int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, in
                        int iters, float *ms, float *pass_ms, int max_pass);
 int hsfft_time_r2c_batched(fft_real_object obj, const fft_type *d_in, fft_data *d_out,
                            int batch, int iters, float *ms);
+/* The drop-in fft_exec on HOST buffers timed in a C loop, as the reference is timed (BASELINE
+ * config 1): `warmup` calls per thread in warm-up threads that then exit, then `nthreads`
+ * (1..64) fresh threads start together and each make `iters` back-to-back fft_exec calls on
+ * `obj` with a private copy of `in` (N complex).  us[0..2]: median, p10 and p90 of thread 0's
+ * per-call latency (microseconds); us[3]: the timed region's wall time / (nthreads x iters),
+ * i.e. microseconds per transform in aggregate.  `out` receives thread 0's last output. */
+int hsfft_time_exec_host(fft_object obj, const fft_data *in, fft_data *out, int nthreads,
+                         int iters, int warmup, double *us);
 
 /* Number of 8-byte words that differ between two device buffers of `bytes` bytes (a multiple
  * of 8) into *count; synchronous.  For whole-output comparisons between schedules (tests). */

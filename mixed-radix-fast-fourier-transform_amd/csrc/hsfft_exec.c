@@ -18,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <ucontext.h>
 #include <unistd.h>
 
@@ -1540,6 +1541,120 @@ int hsfft_fill_real(fft_type *d_x, int64_t count, uint64_t seed, uint64_t offset
 
 static int time_locked(fft_object obj, hs_entry *e, const fft_data *d_in, fft_data *d_out, int batch, int iters,
                        float *ms, float *pass_ms, int max_pass);
+
+/* ------------------------------------------------------------------ drop-in latency in C
+ * BASELINE config 1 (one N = 1024 fft_exec on host buffers) timed the way the reference is
+ * timed -- a C loop of fft_exec calls, no interpreter between calls (bench.py used to time it
+ * through ctypes, ~1 us per call of binding overhead; round 6).  Warm-up threads run first and
+ * exit (their per-thread sets are parked), then `nthreads` fresh threads (which adopt them)
+ * start together on a barrier and each make `iters` calls on the shared plan with their own
+ * copy of the input. */
+/* the timed threads' common start: go 0 wait, 1 run, 2 abandon (a thread could not be created) */
+typedef struct {
+    pthread_mutex_t mtx;
+    pthread_cond_t cv;
+    int go;
+} hs_tx_start;
+
+typedef struct {
+    fft_object obj;
+    const fft_data *in;
+    fft_data *out;
+    int iters, dev;
+    double *lat; /* thread 0: per-call microseconds */
+    hs_tx_start *start;
+} hs_tx_arg;
+
+static double hs_now_us(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static void *hs_tx_worker(void *p)
+{
+    hs_tx_arg *a = (hs_tx_arg *)p;
+    const size_t bytes = sizeof(fft_data) * (size_t)a->obj->N;
+    fft_data *x = (fft_data *)malloc(bytes), *y = (fft_data *)malloc(bytes);
+    if (x) memcpy(x, a->in, bytes);
+    int go = 1;
+    if (a->start) {
+        pthread_mutex_lock(&a->start->mtx);
+        while (a->start->go == 0) pthread_cond_wait(&a->start->cv, &a->start->mtx);
+        go = a->start->go;
+        pthread_mutex_unlock(&a->start->mtx);
+    }
+    if (x && y && go == 1) {
+        (void)hsd_set_device(a->dev);
+        for (int i = 0; i < a->iters; i++) {
+            const double t0 = a->lat ? hs_now_us() : 0.0;
+            fft_exec(a->obj, x, y);
+            if (a->lat) a->lat[i] = hs_now_us() - t0;
+        }
+        if (a->out) memcpy(a->out, y, bytes);
+    }
+    free(x);
+    free(y);
+    return NULL;
+}
+
+static int hs_cmp_double(const void *a, const void *b)
+{
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+int hsfft_time_exec_host(fft_object obj, const fft_data *in, fft_data *out, int nthreads, int iters, int warmup,
+                         double *us)
+{
+    g_errbuf[0] = 0;
+    if (!obj || !in || !out || !us || nthreads < 1 || nthreads > 64 || iters < 1 || warmup < 0) {
+        hs_seterr("hsfft_time_exec_host: invalid arguments");
+        return HSFFT_ERR_ARG;
+    }
+    int rc = hs_require_gpu();
+    if (rc) return rc;
+    const int dev = hsd_get_device();
+    pthread_t th[64];
+    hs_tx_arg args[64];
+    if (warmup > 0) { /* warm-up threads: plan state built, per-thread sets created, then parked */
+        for (int t = 0; t < nthreads; t++) {
+            args[t] = (hs_tx_arg){obj, in, NULL, warmup, dev, NULL, NULL};
+            if (pthread_create(&th[t], NULL, hs_tx_worker, &args[t])) return HSFFT_ERR_NOMEM;
+        }
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    }
+    double *lat = (double *)malloc(sizeof(double) * (size_t)iters);
+    if (!lat) return HSFFT_ERR_NOMEM;
+    hs_tx_start st = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0};
+    int started = 0;
+    for (int t = 0; t < nthreads; t++) {
+        args[t] = (hs_tx_arg){obj, in, t == 0 ? out : NULL, iters, dev, t == 0 ? lat : NULL, &st};
+        if (pthread_create(&th[t], NULL, hs_tx_worker, &args[t])) break;
+        started++;
+    }
+    /* every thread is created (and has copied nothing yet): start them together, or abandon */
+    pthread_mutex_lock(&st.mtx);
+    st.go = started == nthreads ? 1 : 2;
+    pthread_cond_broadcast(&st.cv);
+    pthread_mutex_unlock(&st.mtx);
+    const double t0 = hs_now_us();
+    for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
+    const double wall = hs_now_us() - t0;
+    if (started < nthreads) {
+        free(lat);
+        hs_seterr("hsfft_time_exec_host: thread creation failed");
+        return HSFFT_ERR_NOMEM;
+    }
+    qsort(lat, (size_t)iters, sizeof(double), hs_cmp_double);
+    us[0] = lat[iters / 2];
+    us[1] = lat[iters / 10];
+    us[2] = lat[(size_t)iters * 9 / 10];
+    us[3] = wall / ((double)nthreads * iters);
+    free(lat);
+    return 0;
+}
 
 int hsfft_time_batched(fft_object obj, const fft_data *d_in, fft_data *d_out, int batch, int iters, float *ms,
                        float *pass_ms, int max_pass)

@@ -65,6 +65,7 @@ SIGNATURES = {
     "hsfft_time_batched": (CI, [VP, VP, VP, CI, CI, ctypes.POINTER(ctypes.c_float),
                                 ctypes.POINTER(ctypes.c_float), CI]),
     "hsfft_time_r2c_batched": (CI, [VP, VP, VP, CI, CI, ctypes.POINTER(ctypes.c_float)]),
+    "hsfft_time_exec_host": (CI, [VP, VP, VP, CI, CI, CI, ctypes.POINTER(ctypes.c_double)]),
     "hsfft_exec_multi": (CI, [VP, VP, VP, CI, CI]),
     "hsfft_bench_copy": (CI, [VP, VP, ctypes.c_size_t, CI, ctypes.POINTER(ctypes.c_float)]),
     "hsfft_bluestein_fallbacks": (ctypes.c_longlong, []),

@@ -357,6 +357,18 @@ int main(void)
         CHECK(dr >= 8, "parked sets destroyed by release_scratch: %d", dr);
     }
 
+    { /* the C-loop drop-in timing (bench.py's c1): warm-up threads, then 4 timed threads */
+        fft_object o = fft_init(1024, 1);
+        fft_data *x = cbuf(1024), *y = cbuf(1024);
+        double us[4] = {-1, -1, -1, -1};
+        CHECK(hsfft_time_exec_host(o, x, y, 4, 20, 3, us) == 0, "time_exec_host: %s", hsfft_last_error());
+        CHECK(us[0] >= 0 && us[1] <= us[0] && us[0] <= us[2] && us[3] > 0, "time_exec_host results");
+        CHECK(hsfft_time_exec_host(o, x, y, 0, 20, 3, us) == HSFFT_ERR_ARG, "time_exec_host: 0 threads refused");
+        free(x);
+        free(y);
+        free_fft(o);
+    }
+
     g_shared = fft_init(12600, 1);
     pthread_t th[8];
     for (long t = 0; t < 8; t++) pthread_create(&th[t], NULL, hammer, (void *)t);

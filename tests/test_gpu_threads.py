@@ -196,3 +196,21 @@ def test_thread_generations_recycle_resources():
     assert not errors, errors[:10]
     assert made <= NTHREADS, f"seven generations of {NTHREADS} threads created {made} streams"
     plan.close()
+
+
+@pytest.mark.parametrize("nthreads", [1, 8])
+def test_time_exec_host_c_loop(nthreads):
+    """hsfft_time_exec_host (bench.py's c1 value since round 6: fft_exec in a C loop, as the
+    reference is timed): warm-up threads then fresh timed threads; the output is bit-exact and
+    the statistics are ordered"""
+    import ctypes
+    L = hsfft.lib()
+    n = 1024
+    p = hsfft.Plan(n, 1)
+    x = T.complex_input(n, 0x7800)
+    y = np.zeros(n, dtype=np.complex128)
+    us = (ctypes.c_double * 4)()
+    assert L.hsfft_time_exec_host(p.ptr, T.ptr(x), T.ptr(y), nthreads, 100, 5, us) == 0
+    assert T.bits_equal(y, T.oracle_c2c(x, 1))
+    assert 0 < us[1] <= us[0] <= us[2] and us[3] > 0
+    p.close()
