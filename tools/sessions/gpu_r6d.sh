@@ -7,7 +7,8 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_threads.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r6d_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/r6d_pytest.log; [ $rc = 0 ] || exit $rc
 cat > /tmp/c1d.py <<'PY'
-import sys
+import os, sys
+sys.path.insert(0, os.getcwd())
 sys.argv = ["bench.py"]
 import bench, hsfft
 hsfft.lib().hsfft_set_device(0)
