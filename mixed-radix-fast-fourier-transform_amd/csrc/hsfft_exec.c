@@ -129,9 +129,66 @@ static int pass_pmax(void)
     return v < 8 ? 8 : v;
 }
 
+/* Knob lookups of the small drop-in path (round 6).  fft_exec of N = 1024 on host buffers reads
+ * five HSFFT_* knobs per call, and getenv scans the whole environment each time: measured on the
+ * box, 500 extra environment variables made that call 5.5 us slower (11.6 -> 17.1 us,
+ * profiles/r06d_c1_getenv.txt).  The small path therefore takes one snapshot of the HSFFT_*
+ * entries per call (hs_env_begin), rebuilt only when the environment changed -- the signature
+ * is the `environ` array and the addresses of its strings: setenv / putenv / unsetenv (and
+ * Python's os.environ) replace or move entries, so a changed value changes an address -- and
+ * the lookups inside that call search the snapshot.  Outside such a call hs_getenv is getenv. */
+extern char **environ;
+#define HS_ENV_MAX 64
+static __thread struct {
+    uintptr_t sig;
+    int valid, active, n;
+    const char *kv[HS_ENV_MAX];
+} t_env;
+
+static uintptr_t env_signature(void)
+{
+    uintptr_t h0 = (uintptr_t)environ, h1 = 0;
+    char **e = environ;
+    for (int i = 0; e && e[i]; i++) {
+        if (i & 1) h1 = h1 * 0x9E3779B97F4A7C15ull + (uintptr_t)e[i];
+        else h0 = h0 * 0xC2B2AE3D27D4EB4Full + (uintptr_t)e[i];
+    }
+    return h0 ^ (h1 * 31 + 7);
+}
+
+void hs_env_begin(void)
+{
+    const uintptr_t sig = env_signature();
+    if (!t_env.valid || sig != t_env.sig) {
+        t_env.n = 0;
+        for (char **e = environ; e && *e; e++)
+            if (!strncmp(*e, "HSFFT_", 6)) {
+                if (t_env.n == HS_ENV_MAX) { /* more knobs than the table holds: plain getenv */
+                    t_env.valid = 0;
+                    return;
+                }
+                t_env.kv[t_env.n++] = *e;
+            }
+        t_env.sig = sig;
+        t_env.valid = 1;
+    }
+    t_env.active = 1;
+}
+
+void hs_env_end(void) { t_env.active = 0; }
+
+const char *hs_getenv(const char *name)
+{
+    if (!t_env.active) return getenv(name);
+    const size_t len = strlen(name);
+    for (int i = 0; i < t_env.n; i++)
+        if (!strncmp(t_env.kv[i], name, len) && t_env.kv[i][len] == '=') return t_env.kv[i] + len + 1;
+    return NULL;
+}
+
 static int env_int(const char *name, int dflt)
 {
-    const char *s = getenv(name);
+    const char *s = hs_getenv(name);
     return s ? atoi(s) : dflt;
 }
 
@@ -1346,7 +1403,10 @@ static int small_host_exec_concurrent(fft_object obj, fft_data *inp, fft_data *o
 
 void fft_exec(fft_object obj, fft_data *inp, fft_data *oup)
 {
-    if (small_host_exec_concurrent(obj, inp, oup) == 0) return;
+    hs_env_begin(); /* this call's knob lookups: one snapshot (see hs_getenv) */
+    const int small = small_host_exec_concurrent(obj, inp, oup);
+    hs_env_end();
+    if (small == 0) return;
     const int d = hs_lock_device();
     fft_exec_locked(obj, inp, oup);
     hs_unlock_device(d);

@@ -124,6 +124,10 @@ int hsd_event_wait(int i);
 void *hsd_stream(void);
 int hsd_is_device_ptr(const void *p);
 const char *hsd_errstr(void);
+/* host side (hsfft_exec.c): getenv, served from a per-call snapshot inside the small fft_exec path */
+const char *hs_getenv(const char *name);
+void hs_env_begin(void); /* (the snapshot's scope; tests/sanitize checks its semantics) */
+void hs_env_end(void);
 
 int hsd_run_pass(const hsd_pass *p, const hsd_launch *l);
 /* 1 if the register kernel has an instantiation for [r0, 8^n8] with this tile */

@@ -1160,7 +1160,7 @@ typedef void (*kfn)(Args);
 
 inline int env(const char *name, int dflt)
 {
-    const char *s = getenv(name);
+    const char *s = hs_getenv(name); /* getenv, or the small path's per-call snapshot */
     return s ? atoi(s) : dflt;
 }
 

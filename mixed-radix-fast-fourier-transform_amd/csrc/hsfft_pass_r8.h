@@ -846,7 +846,7 @@ inline int launch(const hsd_pass *p, const hsd_launch *l, hipStream_t st)
         *l->armed = 1;
         /* HSFFT_SMALL_TWA (default 1): the one-workgroup first pass with every stage's twiddles
          * loaded behind its inputs */
-        const char *te = getenv("HSFFT_SMALL_TWA");
+        const char *te = hs_getenv("HSFFT_SMALL_TWA");
         if (first && !hook && p->G == 1 && !(te && atoi(te) == 0))
             for (const Variant &t : k_twa)
                 if (t.r0 == v->r0 && t.n8 == v->n8 && t.split == v->split) v = &t;

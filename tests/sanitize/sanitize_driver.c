@@ -202,8 +202,38 @@ static void *hammer(void *arg)
     return NULL;
 }
 
+/* the small path's per-call snapshot of the HSFFT_* knobs (hs_getenv, round 6): inside a
+ * snapshot scope every lookup equals getenv, after any setenv / unsetenv between scopes too */
+#include "hsfft_internal.h"
+static void check_env_snapshot(void)
+{
+    setenv("HSFFT_ZZ_A", "1", 1);
+    unsetenv("HSFFT_ZZ_B");
+    hs_env_begin();
+    CHECK(hs_getenv("HSFFT_ZZ_A") && !strcmp(hs_getenv("HSFFT_ZZ_A"), "1"), "snapshot: set value");
+    CHECK(hs_getenv("HSFFT_ZZ_B") == NULL && hs_getenv("HSFFT_ZZ") == NULL, "snapshot: absent / prefix");
+    CHECK(hs_getenv("PATH") == NULL, "snapshot: only HSFFT_ knobs");
+    hs_env_end();
+    CHECK(hs_getenv("PATH") == getenv("PATH"), "outside a snapshot: getenv");
+    for (int it = 0; it < 200; it++) {
+        char v[16];
+        snprintf(v, sizeof v, "%d", it % 3); /* values repeat: glibc may reuse a string */
+        setenv("HSFFT_ZZ_A", v, 1);
+        if (it % 5 == 0) setenv("HSFFT_ZZ_B", v, 1);
+        if (it % 7 == 0) unsetenv("HSFFT_ZZ_B");
+        hs_env_begin();
+        const char *a = hs_getenv("HSFFT_ZZ_A"), *b = hs_getenv("HSFFT_ZZ_B"), *gb = getenv("HSFFT_ZZ_B");
+        CHECK(a && !strcmp(a, v), "snapshot after setenv, round %d", it);
+        CHECK((b == NULL) == (gb == NULL) && (!b || !strcmp(b, gb)), "snapshot after unsetenv, round %d", it);
+        hs_env_end();
+    }
+    unsetenv("HSFFT_ZZ_A");
+    unsetenv("HSFFT_ZZ_B");
+}
+
 int main(void)
 {
+    check_env_snapshot();
     for (int n = 1; n <= PLAN_MAX; n++) {
         check_plan(n, 1);
         if (n % 7 == 0) check_plan(n, -1);
