@@ -131,8 +131,8 @@ static int pass_pmax(void)
 
 /* Knob lookups of the small drop-in path (round 6).  fft_exec of N = 1024 on host buffers reads
  * five HSFFT_* knobs per call, and getenv scans the whole environment each time: measured on the
- * box, 500 extra environment variables made that call 5.5 us slower (11.6 -> 17.1 us,
- * profiles/r06d_c1_getenv.txt).  The small path therefore takes one snapshot of the HSFFT_*
+ * box, 500 extra environment variables made that call 5.5 us slower (11.6 -> 17.1 us; with the
+ * snapshot +0.2 us, profiles/r06d_c1_getenv.txt).  The small path therefore takes one snapshot of the HSFFT_*
  * entries per call (hs_env_begin), rebuilt only when the environment changed -- the signature
  * is the `environ` array and the addresses of its strings: setenv / putenv / unsetenv (and
  * Python's os.environ) replace or move entries, so a changed value changes an address -- and
