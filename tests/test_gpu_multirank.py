@@ -5,7 +5,7 @@ ranks select device 0 here (`LOCAL_RANK % device_count`), each transforms its ow
 shard of rows through libhsfft and saves the first and last output row of its shard; every
 saved row must equal the oracle's transform of that GLOBAL row bit for bit, which proves the
 batch-index sharding (no collective) end to end -- for the c2c hot path (config 2) and for the
-chunked r2c path (config 5).  No scaling number is derived from this."""
+chunked r2c path (config 5); and four ranks for c2.  No scaling number is derived from this."""
 import json
 import os
 import subprocess
@@ -21,21 +21,21 @@ import hsfft
 pytestmark = pytest.mark.gpu
 
 
-def run_two_ranks(tmp_path, config, batch, cpu=False):
+def run_two_ranks(tmp_path, config, batch, cpu=False, ranks=2):
     if hsfft.device_count() < 1:
         pytest.skip("no GPU")
     out = tmp_path / "rows"
     env = dict(os.environ, OMP_NUM_THREADS="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(T.REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+    cmd = [sys.executable, os.path.join(T.REPO, "bench.py"), "--gpus", str(ranks), "--steps", "2", "--warmup", "1",
            "--config", config, "--batch", str(batch), "--dump-rows", str(out)]
     cmd += ["--cpu-seconds", "1"] if cpu else ["--no-cpu-baseline"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400, cwd=T.REPO)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1 and lines[0]["n_gpus"] == 2, r.stdout[-2000:]  # rank 0 only, two ranks
-    assert lines[0]["config"]["global_batch"] == 2 * batch
+    assert len(lines) == 1 and lines[0]["n_gpus"] == ranks, r.stdout[-2000:]  # rank 0 only
+    assert lines[0]["config"]["global_batch"] == ranks * batch
     return out, lines[0]
 
 
@@ -75,3 +75,21 @@ def test_two_ranks_r2c_chunked_shard_rows_bit_exact(tmp_path):
             assert T.bits_equal(row, T.oracle_r2c(x, 1)), (rank, int(g))
             seen.add(int(g))
     assert seen == {0, 1, 2, 3}
+
+
+def test_four_ranks_shard_rows_bit_exact(tmp_path):
+    """the 4-rank launch (one step towards the driver's 8-GPU run, rehearsed with four ranks on
+    the one GPU): contiguous shards of 3 rows each, every rank's first and last row bit-exact,
+    four per-rank entries and the aggregate roofline against 4 x the peak"""
+    out, line = run_two_ranks(tmp_path, "c2", 3, ranks=4)
+    assert [p["rank"] for p in line["per_rank"]] == [0, 1, 2, 3]
+    assert line["roofline"]["aggregate"]["peak"] == 32000.0
+    seen = set()
+    for rank in range(4):
+        z = np.load(out / f"rank{rank}.npz")
+        n, seed = int(z["n"]), int(z["seed"])
+        for row, g in zip(z["rows"], z["global_rows"]):
+            x = T.complex_input(n, seed, batch=1, row0=int(g))
+            assert T.bits_equal(row, T.oracle_c2c(x, 1)), (rank, int(g))
+            seen.add(int(g))
+    assert seen == {0, 2, 3, 5, 6, 8, 9, 11}
