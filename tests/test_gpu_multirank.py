@@ -93,3 +93,32 @@ def test_four_ranks_shard_rows_bit_exact(tmp_path):
             assert T.bits_equal(row, T.oracle_c2c(x, 1)), (rank, int(g))
             seen.add(int(g))
     assert seen == {0, 2, 3, 5, 6, 8, 9, 11}
+
+
+def test_one_gpu_line_contract(tmp_path):
+    """the N = 1 bench line carries the contract's fields: metric / value / unit / n_gpus /
+    steps / warmup / ms_per_step / higher_is_better / scaling / vs_baseline / dtype / data /
+    config.workload, `roofline` {bound, achieved, peak, unit, frac, traffic} and `cpu_baseline`
+    {value, unit, cores, kind, sample} (a small batch: traffic is null off the profiled batch)"""
+    if hsfft.device_count() < 1:
+        pytest.skip("no GPU")
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(T.REPO, "bench.py"), "--steps", "2", "--warmup", "1", "--config", "c2",
+           "--batch", "4", "--no-other-configs", "--cpu-seconds", "0.5"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=T.REPO)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0 and d["config"]["workload"]
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0 and "traffic" in rf
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], abs=1e-3)
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["unit"] == "GSamples/s" and cb["cores"] >= 1 and cb["kind"] in ("reference", "port")
+    assert cb["sample"]
