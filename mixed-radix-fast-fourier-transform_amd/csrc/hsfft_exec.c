@@ -1679,11 +1679,16 @@ int hsfft_time_exec_host(fft_object obj, const fft_data *in, fft_data *out, int 
     pthread_t th[64];
     hs_tx_arg args[64];
     if (warmup > 0) { /* warm-up threads: plan state built, per-thread sets created, then parked */
-        for (int t = 0; t < nthreads; t++) {
+        int nw = 0;
+        for (int t = 0; t < nthreads; t++, nw++) {
             args[t] = (hs_tx_arg){obj, in, NULL, warmup, dev, NULL, NULL};
-            if (pthread_create(&th[t], NULL, hs_tx_worker, &args[t])) return HSFFT_ERR_NOMEM;
+            if (pthread_create(&th[t], NULL, hs_tx_worker, &args[t])) break;
         }
-        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+        for (int t = 0; t < nw; t++) pthread_join(th[t], NULL); /* (they use args: joined before any return) */
+        if (nw < nthreads) {
+            hs_seterr("hsfft_time_exec_host: thread creation failed");
+            return HSFFT_ERR_NOMEM;
+        }
     }
     double *lat = (double *)malloc(sizeof(double) * (size_t)iters);
     if (!lat) return HSFFT_ERR_NOMEM;
@@ -1702,6 +1707,8 @@ int hsfft_time_exec_host(fft_object obj, const fft_data *in, fft_data *out, int 
     const double t0 = hs_now_us();
     for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
     const double wall = hs_now_us() - t0;
+    pthread_cond_destroy(&st.cv);
+    pthread_mutex_destroy(&st.mtx);
     if (started < nthreads) {
         free(lat);
         hs_seterr("hsfft_time_exec_host: thread creation failed");
